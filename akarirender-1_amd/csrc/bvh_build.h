@@ -1,0 +1,33 @@
+// bvh_build.h — host binned-SAH builder for the BVH2 of akr_bvh_format.h.
+//
+// Replaces the reference's SBVH build (src/akari/kernel/bvh-accelerator.h:125-475, called from
+// BVHAccelerator::build :673-678).  Closest-hit and occlusion results do not depend on the
+// builder (up to exact ties in t), so the builder is free to target GPU traversal cost:
+// 32-bin SAH per axis (like the reference's nBuckets, :104), no spatial splits (no duplicated
+// references), leaves of at most `max_leaf_size` triangles, task-parallel over std::thread.
+#pragma once
+#include <stdint.h>
+#include <vector>
+#include "../../include/akr_hip.h"
+#include "../../include/akr_bvh_format.h"
+
+namespace akr {
+
+struct BvhInput {
+    const float *vertices;   // 3 * n_vertices
+    const int32_t *indices;  // 3 * n_tris
+    uint64_t n_tris;
+};
+
+struct BvhOutput {
+    std::vector<akr_bvh_node> nodes;
+    std::vector<akr_bvh_tri> tris;
+    int max_depth = 0;
+    int max_leaf = 0;
+    double sah_cost = 0;
+    double build_ms = 0;
+};
+
+void build_bvh(const BvhInput &in, const akr_build_params &params, BvhOutput &out);
+
+}  // namespace akr

@@ -1,0 +1,845 @@
+// capi.hip — implementation of the C-ABI boundary declared in include/akr_hip.h.
+//
+// One context = one device + one stream.  Scene arrays are staged on the host, flattened across
+// meshes (global triangle id = mesh base + prim id) and uploaded once; the BVH is built on the
+// host (bvh_build.cpp) and uploaded.  akr_hip_render runs the wavefront pipeline
+// raygen -> {closest-hit -> shade -> shadow}^depth -> splat once per sample pass, entirely on
+// the stream (no host synchronisation inside a render; queue counts live in device memory).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "akr_device.h"
+#include "bvh_build.h"
+#include "kernels.h"
+
+using namespace akr;
+
+#define HIPCHK(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + " failed: " + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf &) = delete;
+    DBuf &operator=(const DBuf &) = delete;
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void reserve(size_t count) {
+        if (count <= n && p) return;
+        release();
+        size_t c = std::max<size_t>(count, 1);
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&p), c * sizeof(T)));
+        n = c;
+    }
+    void upload(const T *h, size_t count, hipStream_t st) {
+        reserve(count);
+        if (count) HIPCHK(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
+    }
+};
+
+struct Stat {
+    uint64_t launches = 0;
+    double total = 0, mn = 1e30, mx = 0;
+};
+
+// Camera (restated from core/nodes/camera.cpp:26-52 and kernel/camera.h:45-59)
+struct M4 {
+    float m[4][4];
+};
+M4 m_ident() {
+    M4 r{};
+    for (int i = 0; i < 4; i++) r.m[i][i] = 1.0f;
+    return r;
+}
+M4 m_from(const float (&a)[16]) {
+    M4 r;
+    for (int i = 0; i < 16; i++) r.m[i / 4][i % 4] = a[i];
+    return r;
+}
+M4 m_mul(const M4 &a, const M4 &b) {  // Matrix::operator*, math.h:93-101 (sequential dot)
+    M4 r;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            float s = a.m[i][0] * b.m[0][j];
+            s += a.m[i][1] * b.m[1][j];
+            s += a.m[i][2] * b.m[2][j];
+            s += a.m[i][3] * b.m[3][j];
+            r.m[i][j] = s;
+        }
+    return r;
+}
+float hsinf(float x) { return (float)std::sin((double)x); }
+float hcosf(float x) { return (float)std::cos((double)x); }
+M4 m_scale(float x, float y, float z) { return m_from({x, 0, 0, 0, 0, y, 0, 0, 0, 0, z, 0, 0, 0, 0, 1}); }
+M4 m_translate(float x, float y, float z) { return m_from({1, 0, 0, x, 0, 1, 0, y, 0, 0, 1, z, 0, 0, 0, 1}); }
+M4 m_rx(float t) { float s = hsinf(t), c = hcosf(t); return m_from({1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1}); }
+M4 m_ry(float t) { float s = hsinf(t), c = hcosf(t); return m_from({c, 0, s, 0, 0, 1, 0, 0, -s, 0, c, 0, 0, 0, 0, 1}); }
+M4 m_rz(float t) { float s = hsinf(t), c = hcosf(t); return m_from({c, -s, 0, 0, s, c, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}); }
+
+CameraDev make_camera(const akr_camera &c) {
+    const float pi = 3.1415926535897932384f;
+    if (c.resolution[0] <= 0 || c.resolution[1] <= 0 || c.resolution[0] > 65535 || c.resolution[1] > 65535)
+        throw std::runtime_error("camera resolution must be in [1, 65535]");
+    CameraDev cam;
+    cam.width = c.resolution[0];
+    cam.height = c.resolution[1];
+    float rx = c.rotation_deg[0] * pi / 180.0f, ry = c.rotation_deg[1] * pi / 180.0f, rz = c.rotation_deg[2] * pi / 180.0f;
+    M4 c2w = m_rz(rz);
+    c2w = m_mul(m_rx(ry), c2w);
+    c2w = m_mul(m_ry(rx), c2w);
+    c2w = m_mul(m_translate(c.position[0], c.position[1], c.position[2]), c2w);
+    float fov = (float)(c.fov_deg * (double)pi / 180.0);
+    M4 m = m_ident();
+    m = m_mul(m_scale(1.0f / cam.width, 1.0f / cam.height, 1), m);
+    m = m_mul(m_scale(2, 2, 1), m);
+    m = m_mul(m_translate(-1, -1, 0), m);
+    m = m_mul(m_scale(1, -1, 1), m);
+    float s = (float)std::atan((double)(fov / 2));  // atan, not tan (camera.h:51)
+    if (cam.width > cam.height)
+        m = m_mul(m_scale(s, s * float(cam.height) / cam.width, 1), m);
+    else
+        m = m_mul(m_scale(s * float(cam.width) / cam.height, s, 1), m);
+    for (int i = 0; i < 16; i++) {
+        cam.r2c[i] = m.m[i / 4][i % 4];
+        cam.c2w[i] = c2w.m[i / 4][i % 4];
+    }
+    return cam;
+}
+
+}  // namespace
+
+struct akr_hip_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // host staging (flattened over meshes)
+    std::vector<float> verts;
+    std::vector<int32_t> idx;
+    std::vector<float> normals, texcoords;
+    std::vector<int32_t> matid;
+    std::vector<uint32_t> mesh_base{0};
+    std::vector<akr_texture> texs;
+    std::vector<akr_material> mats;
+    std::vector<float> images;
+    std::vector<int64_t> img_off;
+    std::vector<int32_t> img_w, img_h;
+    std::vector<akr_area_light> lights;
+    std::vector<float> power;
+    bool scene_dirty = true;
+    bool accel_built = false;
+    akr_accel_info info{};
+    BvhOutput bvh;
+
+    // device scene
+    DBuf<akr_bvh_node> d_nodes;
+    DBuf<float4> d_tris, d_corner;
+    DBuf<float> d_normals, d_tc, d_images, d_cdf, d_func;
+    DBuf<int32_t> d_matid, d_img_w, d_img_h;
+    DBuf<int64_t> d_img_off;
+    DBuf<akr_material> d_mats;
+    DBuf<akr_texture> d_texs;
+    DBuf<LightDev> d_lights;
+    DBuf<uint32_t> d_mesh_base;
+    float func_int = 0;
+    int32_t n_lights = 0;
+
+    CameraDev cam{};
+    bool cam_set = false;
+
+    // path / queue buffers
+    size_t cap = 0;
+    std::vector<uint32_t> h_pixel;
+    DBuf<uint32_t> d_pixel, d_seed, d_slot0, d_slot1, d_counts;
+    DBuf<float4> d_ray0, d_ray1, d_hit, d_sray, d_scolor, d_beta, d_L, d_film;
+    DBuf<float> d_out_rad, d_out_w;
+    DBuf<uint32_t> d_ovf;
+    uint32_t ovf_threads = 0;
+    uint32_t trace_grid[3] = {0, 0, 0};
+    DBuf<float4> d_trace_rays;
+    DBuf<akr_hit> d_trace_hits;
+
+    // instrumentation
+    bool stats = false, count = false;
+    bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
+    DBuf<TraceCounters> d_counters;
+    std::vector<hipEvent_t> pool;
+    struct Pending {
+        const char *name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::map<std::string, Stat> stat;
+
+    ~akr_hip_ctx() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto &p : pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : pool) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    hipEvent_t event() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        return e;
+    }
+
+    template <class F>
+    void timed(const char *name, hipStream_t st, F &&launch) {
+        if (!stats) {
+            launch();
+            return;
+        }
+        hipEvent_t a = event(), b = event();
+        HIPCHK(hipEventRecord(a, st));
+        launch();
+        HIPCHK(hipEventRecord(b, st));
+        pending.push_back({name, a, b});
+        if (pending.size() > 4096) flush_stats();
+    }
+
+    void flush_stats() {
+        for (auto &p : pending) {
+            HIPCHK(hipEventSynchronize(p.b));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+            Stat &s = stat[p.name];
+            s.launches++;
+            s.total += ms;
+            s.mn = std::min(s.mn, (double)ms);
+            s.mx = std::max(s.mx, (double)ms);
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+
+    SceneDev scene_dev() const {
+        SceneDev s{};
+        s.nodes = d_nodes.p;
+        s.tris = d_tris.p;
+        s.corner = d_corner.p;
+        s.normals = d_normals.p;
+        s.texcoords = d_tc.p;
+        s.matid = d_matid.p;
+        s.mats = d_mats.p;
+        s.texs = d_texs.p;
+        s.images = d_images.p;
+        s.image_off = d_img_off.p;
+        s.image_w = d_img_w.p;
+        s.image_h = d_img_h.p;
+        s.lights = d_lights.p;
+        s.light_cdf = d_cdf.p;
+        s.light_func = d_func.p;
+        s.light_func_int = func_int;
+        s.n_lights = n_lights;
+        s.mesh_base = d_mesh_base.p;
+        s.n_meshes = (int32_t)mesh_base.size() - 1;
+        return s;
+    }
+
+    uint64_t n_tris() const { return matid.size(); }
+
+    void commit_scene() {
+        if (!scene_dirty) return;
+        const uint64_t nt = n_tris();
+        // validate references
+        for (uint64_t g = 0; g < nt; g++)
+            if (matid[g] >= (int32_t)mats.size()) throw std::runtime_error("material index out of range");
+        for (size_t m = 0; m < mats.size(); m++) {
+            const akr_material &x = mats[m];
+            auto tex_ok = [&](int32_t t) { return t >= 0 && t < (int32_t)texs.size(); };
+            auto mat_ok = [&](int32_t t) { return t >= 0 && t < (int32_t)mats.size(); };
+            bool ok = true;
+            if (x.type == AKR_MAT_DIFFUSE || x.type == AKR_MAT_EMISSIVE) ok = tex_ok(x.color);
+            else if (x.type == AKR_MAT_GLOSSY) ok = tex_ok(x.color) && tex_ok(x.roughness);
+            else if (x.type == AKR_MAT_MIX) ok = tex_ok(x.fraction) && mat_ok(x.first) && mat_ok(x.second);
+            else ok = false;
+            if (!ok) throw std::runtime_error("material " + std::to_string(m) + " has an invalid type or reference");
+        }
+        for (auto &t : texs)
+            if (t.type == AKR_TEX_IMAGE && (t.image < 0 || t.image >= (int32_t)img_w.size()))
+                throw std::runtime_error("image texture references a missing image");
+        std::vector<float4> corner(3 * nt);
+        for (uint64_t g = 0; g < nt; g++)
+            for (int k = 0; k < 3; k++) {
+                const float *v = &verts[3 * (size_t)idx[3 * g + k]];
+                corner[3 * g + k] = make_float4(v[0], v[1], v[2], 0.0f);
+            }
+        d_corner.upload(corner.data(), corner.size(), stream);
+        d_normals.upload(normals.data(), normals.size(), stream);
+        d_tc.upload(texcoords.data(), texcoords.size(), stream);
+        d_matid.upload(matid.data(), matid.size(), stream);
+        d_mats.upload(mats.data(), mats.size(), stream);
+        d_texs.upload(texs.data(), texs.size(), stream);
+        d_images.upload(images.data(), images.size(), stream);
+        d_img_off.upload(img_off.data(), img_off.size(), stream);
+        d_img_w.upload(img_w.data(), img_w.size(), stream);
+        d_img_h.upload(img_h.data(), img_h.size(), stream);
+        d_mesh_base.upload(mesh_base.data(), mesh_base.size(), stream);
+        // lights: AreaLight records + Distribution1D over `power` (common/distribution.h:46-64)
+        std::vector<LightDev> ld;
+        for (auto &l : lights) {
+            if (l.geom_id < 0 || l.geom_id + 1 >= (int32_t)mesh_base.size())
+                throw std::runtime_error("light geom_id out of range");
+            uint64_t g = (uint64_t)mesh_base[l.geom_id] + (uint64_t)l.prim_id;
+            if (l.prim_id < 0 || g >= mesh_base[l.geom_id + 1]) throw std::runtime_error("light prim_id out of range");
+            int32_t m = matid[g];
+            if (m < 0 || mats[m].type != AKR_MAT_EMISSIVE) throw std::runtime_error("light triangle is not emissive");
+            LightDev x{};
+            for (int k = 0; k < 3; k++) {
+                const float *v = &verts[3 * (size_t)idx[3 * g + k]];
+                x.v[3 * k + 0] = v[0];
+                x.v[3 * k + 1] = v[1];
+                x.v[3 * k + 2] = v[2];
+                x.tc[2 * k + 0] = texcoords[6 * g + 2 * k + 0];
+                x.tc[2 * k + 1] = texcoords[6 * g + 2 * k + 1];
+            }
+            x.color_tex = mats[m].color;
+            ld.push_back(x);
+        }
+        n_lights = (int32_t)ld.size();
+        std::vector<float> cdf(ld.size() + 1, 0.0f), func(power.begin(), power.end());
+        const size_t n = ld.size();
+        for (size_t i = 0; i < n; i++) cdf[i + 1] = cdf[i] + func[i] / n;
+        func_int = n ? cdf[n] : 0.0f;
+        if (func_int == 0) {
+            for (uint32_t i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n);
+        } else {
+            for (uint32_t i = 1; i < n + 1; ++i) cdf[i] /= func_int;
+        }
+        d_lights.upload(ld.data(), ld.size(), stream);
+        d_cdf.upload(cdf.data(), cdf.size(), stream);
+        d_func.upload(func.data(), func.size(), stream);
+        HIPCHK(hipStreamSynchronize(stream));
+        scene_dirty = false;
+    }
+
+    void ensure_trace_grid() {
+        if (trace_grid[0]) return;
+        uint32_t mx = 0;
+        for (int m = 0; m < 3; m++) {
+            trace_grid[m] = (uint32_t)(n_cu * trace_blocks_per_cu(m));
+            mx = std::max(mx, trace_grid[m]);
+        }
+        ovf_threads = mx * kBlock;
+        d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds) * 2);
+    }
+
+    uint32_t grid_for(int mode, uint64_t n) const {
+        uint64_t need = (n + kBlock - 1) / kBlock;
+        return (uint32_t)std::min<uint64_t>(need, trace_grid[mode]);
+    }
+
+    void ensure_capacity(size_t n) {
+        if (n <= cap) return;
+        d_pixel.reserve(n);
+        d_seed.reserve(n);
+        d_slot0.reserve(n);
+        d_slot1.reserve(n);
+        d_ray0.reserve(2 * n);
+        d_ray1.reserve(2 * n);
+        d_hit.reserve(n);
+        d_sray.reserve(2 * n);
+        d_scolor.reserve(n);
+        d_beta.reserve(n);
+        d_L.reserve(n);
+        d_film.reserve(n);
+        cap = n;
+    }
+
+    TraceArgs trace_args() {
+        TraceArgs t{};
+        t.sc = scene_dev();
+        t.stack_ovf = d_ovf.p;
+        t.ovf_threads = ovf_threads;
+        t.counters = d_counters.p;
+        return t;
+    }
+
+    void require_ready() {
+        if (!accel_built) throw std::runtime_error("acceleration structure not built (call akr_hip_build_accel)");
+        commit_scene();
+        ensure_trace_grid();
+        if (count) {
+            if (!d_counters.p) {
+                d_counters.reserve(3);
+                HIPCHK(hipMemset(d_counters.p, 0, 3 * sizeof(TraceCounters)));
+            }
+        }
+    }
+
+    void trace(const float4 *rays, uint64_t n, akr_hit *hits, int any, hipStream_t st) {
+        require_ready();
+        if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
+        TraceArgs t = trace_args();
+        t.rays = rays;
+        t.n = (uint32_t)n;
+        t.abi_hits = hits;
+        int mode = any ? TRACE_ANY : TRACE_CLOSEST;
+        timed(any ? "trace_any" : "trace_closest", st, [&] { launch_trace(mode, count, !exact_cull, t, grid_for(mode, n), st); });
+        HIPCHK(hipGetLastError());
+    }
+
+    uint64_t render(const akr_pt_params &p, const akr_rect *tiles, int32_t n_tiles, hipStream_t st) {
+        require_ready();
+        if (!cam_set) throw std::runtime_error("camera not set (call akr_hip_set_camera)");
+        if (p.spp < 0 || p.max_depth < 0) throw std::runtime_error("spp and max_depth must be >= 0");
+        if (n_tiles < 0 || (n_tiles > 0 && !tiles)) throw std::runtime_error("invalid tile list");
+        h_pixel.clear();
+        for (int k = 0; k < n_tiles; k++) {
+            int x0 = std::max(0, tiles[k].x0), y0 = std::max(0, tiles[k].y0);
+            int x1 = std::min(cam.width, tiles[k].x1), y1 = std::min(cam.height, tiles[k].y1);
+            for (int y = y0; y < y1; y++)
+                for (int x = x0; x < x1; x++) h_pixel.push_back((uint32_t)x | ((uint32_t)y << 16));
+        }
+        const uint64_t N = h_pixel.size();
+        if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
+        ensure_capacity(N);
+        const int M = p.max_depth + 2;
+        d_counts.reserve(2 * (size_t)M);
+        if (N == 0) return 0;
+        HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
+        const SceneDev sd = scene_dev();
+        const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
+        const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
+                                                             // add nothing: skipped
+        for (int s = 0; s < p.spp; s++) {
+            HIPCHK(hipMemsetAsync(d_counts.p, 0, 2 * (size_t)M * sizeof(uint32_t), st));
+            RaygenArgs rg{};
+            rg.cam = cam;
+            rg.pixel = d_pixel.p;
+            rg.n = (uint32_t)N;
+            rg.seed = d_seed.p;
+            rg.beta = d_beta.p;
+            rg.L = d_L.p;
+            rg.ray_out = d_ray0.p;
+            rg.slot_out = d_slot0.p;
+            rg.count_out = d_counts.p;
+            rg.first_pass = s == 0;
+            timed("raygen", st, [&] { launch_raygen(rg, st); });
+            for (int b = 0; b < nb; b++) {
+                float4 *rin = (b & 1) ? d_ray1.p : d_ray0.p;
+                float4 *rout = (b & 1) ? d_ray0.p : d_ray1.p;
+                uint32_t *sin_ = (b & 1) ? d_slot1.p : d_slot0.p;
+                uint32_t *sout = (b & 1) ? d_slot0.p : d_slot1.p;
+                TraceArgs t = trace_args();
+                t.rays = rin;
+                t.count = d_counts.p + b;
+                t.hits = d_hit.p;
+                timed("trace_closest", st, [&] { launch_trace(TRACE_CLOSEST, count, tight, t, grid_for(TRACE_CLOSEST, N), st); });
+                ShadeArgs sh{};
+                sh.sc = sd;
+                sh.ray_in = rin;
+                sh.slot_in = sin_;
+                sh.hit_in = d_hit.p;
+                sh.count_in = d_counts.p + b;
+                sh.ray_out = rout;
+                sh.slot_out = sout;
+                sh.count_out = d_counts.p + b + 1;
+                sh.shadow_ray = d_sray.p;
+                sh.shadow_color = d_scolor.p;
+                sh.shadow_count = d_counts.p + M + b;
+                sh.seed = d_seed.p;
+                sh.beta = d_beta.p;
+                sh.L = d_L.p;
+                sh.depth = b;
+                sh.max_depth = p.max_depth;
+                sh.capacity = (uint32_t)N;
+                timed("shade", st, [&] { launch_shade(sh, (uint32_t)N, st); });
+                if (b < p.max_depth) {
+                    TraceArgs ts = trace_args();
+                    ts.rays = d_sray.p;
+                    ts.count = d_counts.p + M + b;
+                    ts.shadow_color = d_scolor.p;
+                    ts.L = d_L.p;
+                    timed("trace_shadow", st, [&] { launch_trace(TRACE_SHADOW, count, tight, ts, grid_for(TRACE_SHADOW, N), st); });
+                }
+            }
+            SplatArgs sp{};
+            sp.L = d_L.p;
+            sp.film = d_film.p;
+            sp.n = (uint32_t)N;
+            sp.ray_clamp = p.ray_clamp;
+            timed("splat", st, [&] { launch_splat(sp, st); });
+        }
+        HIPCHK(hipGetLastError());
+        return N;
+    }
+};
+
+namespace {
+
+template <class F>
+int guard(akr_hip_ctx *ctx, F &&f) {
+    if (!ctx) return -1;
+    try {
+        HIPCHK(hipSetDevice(ctx->device));
+        f();
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -1;
+    } catch (...) {
+        ctx->err = "unknown error";
+        return -1;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int akr_hip_api_version(void) { return AKR_HIP_API_VERSION; }
+
+int akr_hip_device_count(int *n) {
+    if (!n) return -1;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return 0;
+}
+
+int akr_hip_create(int device, akr_hip_ctx **out) {
+    if (!out) return -1;
+    *out = nullptr;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) return -2;
+    std::unique_ptr<akr_hip_ctx> ctx(new (std::nothrow) akr_hip_ctx());
+    if (!ctx) return -1;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess) return -1;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return -1;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->n_cu = prop.multiProcessorCount;
+    *out = ctx.release();
+    return 0;
+}
+
+int akr_hip_destroy(akr_hip_ctx *ctx) {
+    delete ctx;
+    return 0;
+}
+
+const char *akr_hip_last_error(const akr_hip_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
+    return guard(ctx, [&] {
+        std::string k = key ? key : "";
+        if (k == "stats") {
+            ctx->stats = value != 0;
+        } else if (k == "exact_cull") {
+            ctx->exact_cull = value != 0;
+        } else if (k == "count_tests") {
+            ctx->count = value != 0;
+        } else {
+            throw std::runtime_error("unknown option '" + k + "'");
+        }
+    });
+}
+
+int akr_hip_upload_mesh(akr_hip_ctx *ctx, const float *vertices, uint64_t n_vertices, const int32_t *indices,
+                        const float *normals, const float *texcoords, const int32_t *material_indices,
+                        uint64_t n_triangles, const int32_t *material_slots, int32_t n_slots, int32_t *geom_id) {
+    return guard(ctx, [&] {
+        if (n_triangles && (!vertices || !indices || !normals || !texcoords || !material_indices))
+            throw std::runtime_error("null mesh array");
+        if (ctx->n_tris() + n_triangles >= (1ull << 31)) throw std::runtime_error("scene too large");
+        const uint64_t vb = ctx->verts.size() / 3;
+        for (uint64_t i = 0; i < 3 * n_triangles; i++)
+            if (indices[i] < 0 || (uint64_t)indices[i] >= n_vertices) throw std::runtime_error("vertex index out of range");
+        for (uint64_t t = 0; t < n_triangles; t++) {
+            int32_t m = material_indices[t];
+            if (m >= n_slots) throw std::runtime_error("material index beyond the mesh's material list");
+        }
+        ctx->verts.insert(ctx->verts.end(), vertices, vertices + 3 * n_vertices);
+        for (uint64_t i = 0; i < 3 * n_triangles; i++) ctx->idx.push_back((int32_t)(indices[i] + vb));
+        ctx->normals.insert(ctx->normals.end(), normals, normals + 9 * n_triangles);
+        ctx->texcoords.insert(ctx->texcoords.end(), texcoords, texcoords + 6 * n_triangles);
+        for (uint64_t t = 0; t < n_triangles; t++) {
+            int32_t m = material_indices[t];
+            ctx->matid.push_back(m < 0 ? -1 : material_slots[m]);  // -1: no material (scene.h:73-76)
+        }
+        if (geom_id) *geom_id = (int32_t)ctx->mesh_base.size() - 1;
+        ctx->mesh_base.push_back((uint32_t)ctx->n_tris());
+        ctx->scene_dirty = true;
+        ctx->accel_built = false;
+    });
+}
+
+int akr_hip_upload_images(akr_hip_ctx *ctx, const float *rgba, const int32_t *widths, const int32_t *heights,
+                          int32_t n_images) {
+    return guard(ctx, [&] {
+        ctx->images.clear();
+        ctx->img_off.clear();
+        ctx->img_w.clear();
+        ctx->img_h.clear();
+        int64_t off = 0;
+        for (int i = 0; i < n_images; i++) {
+            if (widths[i] <= 0 || heights[i] <= 0) throw std::runtime_error("empty image");
+            ctx->img_off.push_back(off);
+            ctx->img_w.push_back(widths[i]);
+            ctx->img_h.push_back(heights[i]);
+            off += 4 * (int64_t)widths[i] * heights[i];
+        }
+        ctx->images.assign(rgba, rgba + off);
+        ctx->scene_dirty = true;
+    });
+}
+
+int akr_hip_upload_textures(akr_hip_ctx *ctx, const akr_texture *textures, int32_t n) {
+    return guard(ctx, [&] {
+        ctx->texs.assign(textures, textures + n);
+        ctx->scene_dirty = true;
+    });
+}
+
+int akr_hip_upload_materials(akr_hip_ctx *ctx, const akr_material *materials, int32_t n) {
+    return guard(ctx, [&] {
+        ctx->mats.assign(materials, materials + n);
+        ctx->scene_dirty = true;
+    });
+}
+
+int akr_hip_upload_lights(akr_hip_ctx *ctx, const akr_area_light *lights, int32_t n, const float *power) {
+    return guard(ctx, [&] {
+        if (n < 0 || (n > 0 && (!lights || !power))) throw std::runtime_error("invalid light list");
+        ctx->lights.assign(lights, lights + n);
+        ctx->power.assign(power, power + n);
+        ctx->scene_dirty = true;
+    });
+}
+
+int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
+    return guard(ctx, [&] {
+        akr_build_params p{};
+        p.max_leaf_size = 4;
+        p.n_bins = 32;
+        p.traversal_cost = 1.0f;
+        p.intersect_cost = 1.0f;
+        if (params) p = *params;
+        BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
+        build_bvh(in, p, ctx->bvh);
+        auto &b = ctx->bvh;
+        ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
+        ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        ctx->info.n_nodes = b.nodes.size();
+        ctx->info.n_tris = b.tris.size();
+        ctx->info.max_depth = b.max_depth;
+        ctx->info.max_leaf = b.max_leaf;
+        ctx->info.build_ms = b.build_ms;
+        ctx->info.sah_cost = b.sah_cost;
+        ctx->accel_built = true;
+        ctx->commit_scene();
+    });
+}
+
+int akr_hip_accel_info(akr_hip_ctx *ctx, akr_accel_info *info) {
+    return guard(ctx, [&] {
+        if (!ctx->accel_built) throw std::runtime_error("acceleration structure not built");
+        *info = ctx->info;
+    });
+}
+
+int akr_hip_accel_export(akr_hip_ctx *ctx, void *nodes, uint64_t node_bytes, void *tris, uint64_t tri_bytes) {
+    return guard(ctx, [&] {
+        if (!ctx->accel_built) throw std::runtime_error("acceleration structure not built");
+        uint64_t nb = ctx->bvh.nodes.size() * sizeof(akr_bvh_node), tb = ctx->bvh.tris.size() * sizeof(akr_bvh_tri);
+        if (node_bytes < nb || tri_bytes < tb) throw std::runtime_error("export buffers too small");
+        std::memcpy(nodes, ctx->bvh.nodes.data(), nb);
+        std::memcpy(tris, ctx->bvh.tris.data(), tb);
+    });
+}
+
+int akr_hip_set_camera(akr_hip_ctx *ctx, const akr_camera *camera) {
+    return guard(ctx, [&] {
+        if (!camera) throw std::runtime_error("null camera");
+        ctx->cam = make_camera(*camera);
+        ctx->cam_set = true;
+    });
+}
+
+int akr_hip_trace(akr_hip_ctx *ctx, const akr_ray *rays, uint64_t n, akr_hit *hits, int any_hit) {
+    return guard(ctx, [&] {
+        if (n == 0) return;
+        if (!rays || !hits) throw std::runtime_error("null ray or hit buffer");
+        static_assert(sizeof(akr_ray) == 2 * sizeof(float4), "akr_ray layout");
+        ctx->d_trace_rays.upload(reinterpret_cast<const float4 *>(rays), 2 * n, ctx->stream);
+        ctx->d_trace_hits.reserve(n);
+        ctx->trace(ctx->d_trace_rays.p, n, ctx->d_trace_hits.p, any_hit, ctx->stream);
+        HIPCHK(hipMemcpyAsync(hits, ctx->d_trace_hits.p, n * sizeof(akr_hit), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int akr_hip_trace_device(akr_hip_ctx *ctx, const void *d_rays, uint64_t n, void *d_hits, int any_hit, void *stream) {
+    return guard(ctx, [&] {
+        if (n == 0) return;
+        if (!d_rays || !d_hits) throw std::runtime_error("null ray or hit buffer");
+        hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+        ctx->trace(reinterpret_cast<const float4 *>(d_rays), n, reinterpret_cast<akr_hit *>(d_hits), any_hit, st);
+    });
+}
+
+int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles, int32_t n_tiles,
+                   float *radiance, float *weight) {
+    return guard(ctx, [&] {
+        if (!params || !radiance || !weight) throw std::runtime_error("null argument");
+        hipStream_t st = ctx->stream;
+        uint64_t N = ctx->render(*params, tiles, n_tiles, st);
+        if (N == 0) return;
+        std::vector<float4> film(N);
+        HIPCHK(hipMemcpyAsync(film.data(), ctx->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const int W = ctx->cam.width;
+        for (uint64_t k = 0; k < N; k++) {  // Film::merge_tile (core/film.h:85-95)
+            uint32_t px = ctx->h_pixel[k];
+            uint64_t pix = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
+            radiance[3 * pix + 0] += film[k].x;
+            radiance[3 * pix + 1] += film[k].y;
+            radiance[3 * pix + 2] += film[k].z;
+            weight[pix] += film[k].w;
+        }
+    });
+}
+
+int akr_hip_render_device(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles, int32_t n_tiles,
+                          float *d_radiance, float *d_weight, void *stream, uint64_t *n_pixels) {
+    return guard(ctx, [&] {
+        if (!params || !d_radiance || !d_weight) throw std::runtime_error("null argument");
+        hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+        uint64_t N = ctx->render(*params, tiles, n_tiles, st);
+        if (n_pixels) *n_pixels = N;
+        ctx->timed("unpack", st, [&] { launch_unpack(ctx->d_film.p, (uint32_t)N, d_radiance, d_weight, st); });
+        HIPCHK(hipGetLastError());
+    });
+}
+
+struct akr_bvh_host {
+    BvhOutput out;
+};
+
+int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t *indices, uint64_t n_triangles,
+                       const akr_build_params *params, akr_bvh_host **out, akr_accel_info *info) {
+    if (!out) return -1;
+    *out = nullptr;
+    try {
+        for (uint64_t i = 0; i < 3 * n_triangles; i++)
+            if (indices[i] < 0 || (uint64_t)indices[i] >= n_vertices) return -1;
+        akr_build_params p{};
+        p.max_leaf_size = 4;
+        p.n_bins = 32;
+        p.traversal_cost = 1.0f;
+        p.intersect_cost = 1.0f;
+        if (params) p = *params;
+        std::unique_ptr<akr_bvh_host> h(new akr_bvh_host());
+        BvhInput in{vertices, indices, n_triangles};
+        build_bvh(in, p, h->out);
+        if (info) {
+            info->n_nodes = h->out.nodes.size();
+            info->n_tris = h->out.tris.size();
+            info->max_depth = h->out.max_depth;
+            info->max_leaf = h->out.max_leaf;
+            info->build_ms = h->out.build_ms;
+            info->sah_cost = h->out.sah_cost;
+        }
+        *out = h.release();
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+const void *akr_bvh_host_nodes(const akr_bvh_host *h) { return h ? h->out.nodes.data() : nullptr; }
+const void *akr_bvh_host_tris(const akr_bvh_host *h) { return h ? h->out.tris.data() : nullptr; }
+void akr_bvh_host_free(akr_bvh_host *h) { delete h; }
+
+int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n) {
+    return guard(ctx, [&] {
+        ctx->flush_stats();
+        int32_t k = 0;
+        for (auto &kv : ctx->stat) {
+            if (k < max_n && out) {
+                akr_kernel_stat &s = out[k];
+                std::memset(&s, 0, sizeof(s));
+                std::strncpy(s.name, kv.first.c_str(), sizeof(s.name) - 1);
+                s.launches = kv.second.launches;
+                s.total_ms = kv.second.total;
+                s.min_ms = kv.second.launches ? kv.second.mn : 0;
+                s.max_ms = kv.second.mx;
+            }
+            k++;
+        }
+        if (n) *n = k;
+    });
+}
+
+int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
+    return guard(ctx, [&] {
+        std::memset(out, 0, sizeof(*out));
+        if (!ctx->d_counters.p) return;
+        HIPCHK(hipDeviceSynchronize());
+        TraceCounters c[3];
+        HIPCHK(hipMemcpy(c, ctx->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
+        out->rays = c[0].rays + c[1].rays + c[2].rays;
+        out->box_tests = c[0].box + c[1].box + c[2].box;
+        out->tri_tests = c[0].tri + c[1].tri + c[2].tri;
+        out->closest_rays = c[0].rays;
+        out->shadow_rays = c[1].rays + c[2].rays;
+        for (int m = 0; m < 3; m++) {
+            out->per_mode[m][0] = c[m].rays;
+            out->per_mode[m][1] = c[m].box;
+            out->per_mode[m][2] = c[m].tri;
+        }
+    });
+}
+
+int akr_hip_reset_stats(akr_hip_ctx *ctx) {
+    return guard(ctx, [&] {
+        HIPCHK(hipDeviceSynchronize());
+        ctx->flush_stats();
+        ctx->stat.clear();
+        if (ctx->d_counters.p) HIPCHK(hipMemset(ctx->d_counters.p, 0, 3 * sizeof(TraceCounters)));
+    });
+}
+
+int akr_hip_synchronize(akr_hip_ctx *ctx) {
+    return guard(ctx, [&] {
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipDeviceSynchronize());
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,541 @@
+// kernels.hip — hand-written gfx950 kernels of the wavefront path tracer.
+//
+//   k_trace<CLOSEST|ANY>  BVH2 traversal, one ray per lane, LDS-resident stack
+//                         (TBVHAccelerator::intersect / occlude, bvh-accelerator.h:488-547)
+//   k_raygen              camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86)
+//   k_shade               hit -> emission / BSDF sample / NEE light sample, wave-ballot compaction
+//                         of live paths and shadow rays (pathtracer.h:69-132)
+//   k_splat               Tile::add_sample per slot (core/film.h:66-70)
+//
+// Numerics: f32 with the reference's operation order (akr_math.h); the library is built with
+// -ffp-contract=off and correctly rounded division/sqrt.
+#include "akr_device.h"
+#include "akr_math.h"
+#include "kernels.h"
+
+namespace akr {
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
+
+// intersectAABB (bvh-accelerator.h:89-103); returns -1 on a miss.  The reference accepts every
+// box whose slab interval is non-empty and starts before tmax — including boxes that lie wholly
+// BEHIND the origin (exit m1 < tmin).  TIGHT additionally requires t <= m1 (the standard slab
+// test): it culls only boxes that cannot contain a hit with t > tmin, so it changes which nodes
+// are visited, never which triangle is the closest hit.
+template <bool TIGHT>
+__device__ __forceinline__ float box_test(float lox, float hix, float loy, float hiy, float loz, float hiz, V3 o,
+                                          V3 invd, float tmin, float tmax) {
+    float t0x = (lox - o.x) * invd.x, t1x = (hix - o.x) * invd.x;
+    float t0y = (loy - o.y) * invd.y, t1y = (hiy - o.y) * invd.y;
+    float t0z = (loz - o.z) * invd.z, t1z = (hiz - o.z) * invd.z;
+    float m0 = rmax(rmax(rmin(t0x, t1x), rmin(t0y, t1y)), rmin(t0z, t1z));
+    float m1 = rmin(rmin(rmax(t0x, t1x), rmax(t0y, t1y)), rmax(t0z, t1z));
+    float t = rmax(tmin, m0);
+    bool hit = m0 <= m1 && !(t >= tmax);
+    if (TIGHT) hit = hit && t <= m1;
+    return hit ? t : -1.0f;
+}
+
+// MeshInstance::intersect (instance.h:42-80), Moller-Trumbore on a leaf record (v0, e1, e2).
+__device__ __forceinline__ bool mt(V3 o, V3 d, float tmin, float tmax, float4 a, float4 b, float4 c, float best,
+                                   float &tout, float &uout, float &vout) {
+    V3 v0{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
+    V3 h = cross(d, e2);
+    float det = dot(e1, h);
+    if (det > -1e-6f && det < 1e-6f) return false;
+    float f = 1.0f / det;
+    V3 s = sub(o, v0);
+    float u = f * dot(s, h);
+    if (u < 0.0f || u > 1.0f) return false;
+    V3 q = cross(s, e1);
+    float v = f * dot(d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    float t = f * dot(e2, q);
+    if (t > tmin && t < tmax && t < best) {
+        tout = t;
+        uout = u;
+        vout = v;
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Reserve `want ? 1 : 0` slots per lane of a converged wave: ballot + mbcnt prefix, one atomic.
+__device__ __forceinline__ uint32_t wave_append(bool want, uint32_t *counter) {
+    unsigned long long m = __ballot(want);
+    uint32_t prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    uint32_t cnt = (uint32_t)__popcll(m);
+    unsigned long long act = __ballot(1);
+    int leader = __ffsll((long long)act) - 1;
+    uint32_t base = 0;
+    if ((int)__lane_id() == leader && cnt) base = atomicAdd(counter, cnt);
+    base = __shfl(base, leader);
+    return base + prefix;
+}
+
+// ------------------------------------------------------------------------------------- trace
+// One ray per lane.  The reference processes a node by testing its own box when it is popped;
+// here a node's two child boxes are tested when the node is visited and the far child is pushed
+// with its entry distance, which is re-compared against the current best t when popped.  Both
+// give the same visit order (near = left iff d[axis] > 0) and the same culling, hence the same
+// result as the reference traversal over the same tree.
+template <int MODE, bool COUNT, bool TIGHT>
+__global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
+    constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
+    __shared__ uint32_t s_ref[kStackLds * kBlock];
+    __shared__ float s_t[kStackLds * kBlock];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gtid = blockIdx.x * kBlock + tid;
+    const uint32_t stride = gridDim.x * kBlock;
+    const uint32_t n = a.count ? *a.count : a.n;
+    const uint4 *nodes = reinterpret_cast<const uint4 *>(a.sc.nodes);
+    const float4 *nodesf = reinterpret_cast<const float4 *>(a.sc.nodes);
+    unsigned long long c_rays = 0, c_box = 0, c_tri = 0;
+
+    // virtual root (node 0): child 0 = real root with its box
+    const float4 r0 = nodesf[0], r2 = nodesf[2];
+    const uint4 r3 = nodes[3];
+
+    for (uint32_t i = gtid; i < n; i += stride) {
+        const float4 ra = a.rays[2 * (size_t)i], rb = a.rays[2 * (size_t)i + 1];
+        const V3 o{ra.x, ra.y, ra.z}, d{rb.x, rb.y, rb.z};
+        const float tmin = ra.w, tmax = rb.w;
+        const V3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        float best = kInf, bu = 0.0f, bv = 0.0f;
+        uint32_t bgid = kNoHit;
+        bool occluded = false;
+        int sp = 0;
+        uint32_t cur = r3.x;
+        if (COUNT) { c_rays++; c_box++; }
+        float troot = box_test<TIGHT>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+        bool alive = (cur != AKR_CHILD_EMPTY) && !(troot < 0.0f || troot > (ANY ? tmax : best));
+        while (alive) {
+            if (!(cur & AKR_CHILD_LEAF)) {
+                const float4 q0 = nodesf[4 * (size_t)cur + 0];
+                const float4 q1 = nodesf[4 * (size_t)cur + 1];
+                const float4 q2 = nodesf[4 * (size_t)cur + 2];
+                const uint4 q3 = nodes[4 * (size_t)cur + 3];
+                if (COUNT) c_box += 2;
+                const float t0 = box_test<TIGHT>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
+                const float t1 = box_test<TIGHT>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
+                const float lim = ANY ? tmax : best;
+                const bool p0 = !(t0 < 0.0f || t0 > lim);
+                const bool p1 = !(t1 < 0.0f || t1 > lim);
+                const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
+                const bool left_first = dax > 0;
+                const uint32_t near_ref = left_first ? q3.x : q3.y;
+                const uint32_t far_ref = left_first ? q3.y : q3.x;
+                const bool pn = left_first ? p0 : p1;
+                const bool pf = left_first ? p1 : p0;
+                const float tf = left_first ? t1 : t0;
+                if (pn) {
+                    if (pf) {
+                        if (sp < kStackLds) {
+                            s_ref[sp * kBlock + tid] = far_ref;
+                            s_t[sp * kBlock + tid] = tf;
+                        } else {
+                            size_t e = ((size_t)(sp - kStackLds) * a.ovf_threads + gtid) * 2;
+                            a.stack_ovf[e] = far_ref;
+                            a.stack_ovf[e + 1] = fbits(tf);
+                        }
+                        sp++;
+                    }
+                    cur = near_ref;
+                    continue;
+                }
+                if (pf) {
+                    cur = far_ref;
+                    continue;
+                }
+            } else {
+                const uint32_t first = akr_leaf_first(cur), cnt = akr_leaf_count(cur);
+                for (uint32_t k = 0; k < cnt; k++) {
+                    const float4 ta = a.sc.tris[3 * (size_t)(first + k) + 0];
+                    const float4 tb = a.sc.tris[3 * (size_t)(first + k) + 1];
+                    const float4 tc = a.sc.tris[3 * (size_t)(first + k) + 2];
+                    if (COUNT) c_tri++;
+                    float t, u, v;
+                    if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
+                        best = t;
+                        bu = u;
+                        bv = v;
+                        bgid = fbits(ta.w);
+                        if (ANY) {
+                            occluded = true;
+                            break;
+                        }
+                    }
+                }
+                if (ANY && occluded) break;
+            }
+            // pop, re-checking the stored entry distance against the current best
+            alive = false;
+            while (sp > 0) {
+                --sp;
+                uint32_t r;
+                float tt;
+                if (sp < kStackLds) {
+                    r = s_ref[sp * kBlock + tid];
+                    tt = s_t[sp * kBlock + tid];
+                } else {
+                    size_t e = ((size_t)(sp - kStackLds) * a.ovf_threads + gtid) * 2;
+                    r = a.stack_ovf[e];
+                    tt = bitsf(a.stack_ovf[e + 1]);
+                }
+                if (!(tt > (ANY ? tmax : best))) {
+                    cur = r;
+                    alive = true;
+                    break;
+                }
+            }
+        }
+        if (MODE == TRACE_SHADOW) {
+            if (!occluded) {
+                const float4 c = a.shadow_color[i];
+                const uint32_t slot = fbits(c.w);
+                float4 l = a.L[slot];
+                l.x += c.x;
+                l.y += c.y;
+                l.z += c.z;
+                a.L[slot] = l;
+            }
+        } else if (a.abi_hits) {
+            akr_hit h;
+            bool hit = ANY ? occluded : (bgid != kNoHit);
+            h.t = hit ? best : kInf;
+            h.u = hit ? bu : 0.0f;
+            h.v = hit ? bv : 0.0f;
+            h.geom_id = -1;
+            h.prim_id = -1;
+            if (hit) {
+                int lo = 0, hi = a.sc.n_meshes;  // largest m with mesh_base[m] <= gid
+                while (hi - lo > 1) {
+                    int mid = (lo + hi) / 2;
+                    if (a.sc.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
+                }
+                h.geom_id = lo;
+                h.prim_id = (int32_t)(bgid - a.sc.mesh_base[lo]);
+            }
+            h._pad[0] = h._pad[1] = h._pad[2] = 0;
+            a.abi_hits[i] = h;
+        } else {
+            a.hits[i] = make_float4(best, bu, bv, bitsf(bgid));
+        }
+    }
+    if (COUNT) {
+        c_rays = wave_sum(c_rays);
+        c_box = wave_sum(c_box);
+        c_tri = wave_sum(c_tri);
+        if (__lane_id() == 0) {
+            atomicAdd(&a.counters[MODE].rays, c_rays);
+            atomicAdd(&a.counters[MODE].box, c_box);
+            atomicAdd(&a.counters[MODE].tri, c_tri);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ raygen
+__device__ __forceinline__ void apply_rows(const float *m, float x, float y, float z, float w, float *r, int rows) {
+    for (int i = 0; i < rows; i++) {
+        float s = m[4 * i + 0] * x;
+        s += m[4 * i + 1] * y;
+        s += m[4 * i + 2] * z;
+        s += m[4 * i + 3] * w;
+        r[i] = s;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t px = a.pixel[i];
+    const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
+    uint32_t seed = a.first_pass ? (uint32_t)(x + y * a.cam.width) : a.seed[i];
+    // camera_ray: generate_ray(next2d() /*lens*/, next2d() /*film*/, p) — pathtracer.h:61-64
+    lcg_next2(seed);
+    const V2 u2 = lcg_next2(seed);
+    const float pfx = (float)x + u2.x, pfy = (float)y + u2.y;
+    float r[4];
+    apply_rows(a.cam.r2c, pfx, pfy, 0.0f, 1.0f, r, 4);  // Transform::apply_point, math.h:243-251
+    float px_ = r[0], py_ = r[1];
+    if (r[3] != 1.0f) {
+        px_ = px_ / r[3];
+        py_ = py_ / r[3];
+    }
+    V3 d = normalize(v3(px_ - 0.0f, py_ - 0.0f, 0.0f - 1.0f));
+    float ro[4];
+    apply_rows(a.cam.c2w, 0.0f, 0.0f, 0.0f, 1.0f, ro, 4);
+    V3 o = v3(ro[0], ro[1], ro[2]);
+    if (ro[3] != 1.0f) o = divs(o, ro[3]);
+    float rd[3];
+    for (int k = 0; k < 3; k++) {  // apply_vector: m3 * v, math.h:253
+        float s = a.cam.c2w[4 * k + 0] * d.x;
+        s += a.cam.c2w[4 * k + 1] * d.y;
+        s += a.cam.c2w[4 * k + 2] * d.z;
+        rd[k] = s;
+    }
+    a.seed[i] = seed;
+    a.beta[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    a.L[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a.ray_out[2 * (size_t)i] = make_float4(o.x, o.y, o.z, kEps);
+    a.ray_out[2 * (size_t)i + 1] = make_float4(rd[0], rd[1], rd[2], kInf);
+    a.slot_out[i] = i;
+    if (i == 0) *a.count_out = a.n;
+}
+
+// ------------------------------------------------------------------------------------- shade
+// Texture::evaluate (texture.h:30-66; image lookup core/image.hpp:83-99)
+__device__ __forceinline__ V3 tex_eval(const SceneDev &s, int32_t ti, V2 tc) {
+    const akr_texture t = s.texs[ti];
+    if (t.type == AKR_TEX_CONSTANT) return v3(t.value[0], t.value[1], t.value[2]);
+    float x = fmodf(tc.x, 1.0f);
+    float y = 1.0f - fmodf(tc.y, 1.0f);
+    const int w = s.image_w[t.image], h = s.image_h[t.image];
+    int ix = (int)(x * (float)w), iy = (int)(y * (float)h);
+    ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
+    const float *p = s.images + s.image_off[t.image] + 4 * ((int64_t)ix + (int64_t)iy * w);
+    return v3(p[0], p[1], p[2]);
+}
+
+__device__ __forceinline__ V3 ld3(const float *p) { return v3(p[0], p[1], p[2]); }
+
+// One bounce of GenericPathTracer::run_megakernel for every queued hit (pathtracer.h:137-162):
+// on_surface_scatter (:96-132) then compute_direct_lighting(select_light) (:65-91).
+__global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = *a.count_in;
+    bool want_ext = false, want_sh = false;
+    float4 e0 = {}, e1 = {}, s0 = {}, s1 = {}, sc = {};
+    uint32_t slot = 0;
+    if (i < n) {
+        slot = a.slot_in[i];
+        const float4 hv = a.hit_in[i];
+        const uint32_t gid = fbits(hv.w);
+        const int32_t mid = gid != kNoHit ? a.sc.matid[gid] : -1;
+        if (mid >= 0) {  // miss -> on_miss (no-op); null material terminates (undefined in ref)
+            const SceneDev &s = a.sc;
+            const float4 rdv = a.ray_in[2 * (size_t)i + 1];
+            const V3 wo = neg(v3(rdv.x, rdv.y, rdv.z));
+            const float u = hv.y, v = hv.z;
+            const float4 c0 = s.corner[3 * (size_t)gid + 0];
+            const float4 c1 = s.corner[3 * (size_t)gid + 1];
+            const float4 c2 = s.corner[3 * (size_t)gid + 2];
+            const V3 v0{c0.x, c0.y, c0.z}, v1{c1.x, c1.y, c1.z}, v2{c2.x, c2.y, c2.z};
+            // SurfaceInteraction(uv, triangle) (interaction.h:40-41, shape.h:31-40)
+            const V3 p = lerp3(v0, v1, v2, u, v);
+            const V3 ng = normalize(cross(sub(v1, v0), sub(v2, v0)));
+            const float *nn = s.normals + 9 * (size_t)gid;
+            const V3 ns = lerp3(ld3(nn), ld3(nn + 3), ld3(nn + 6), u, v);
+            const float *tt = s.texcoords + 6 * (size_t)gid;
+            const V2 tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
+            const akr_material *mat = &s.mats[mid];
+            uint32_t seed = a.seed[slot];
+            const float4 bv = a.beta[slot];
+            const V3 beta{bv.x, bv.y, bv.z};
+            if (mat->type == AKR_MAT_EMISSIVE) {
+                if (a.depth == 0) {
+                    const bool face_front = dot(neg(wo), ng) < 0.0f;
+                    if (mat->double_sided || face_front) {
+                        const V3 e = mul(beta, tex_eval(s, mat->color, tc));
+                        float4 l = a.L[slot];
+                        l.x += e.x;
+                        l.y += e.y;
+                        l.z += e.z;
+                        a.L[slot] = l;
+                    }
+                }
+            } else if (a.depth < a.max_depth) {
+                // MaterialEvalContext holds a COPY of the sampler: u1.x is the next draw
+                uint32_t copy = seed;
+                float sel_u = lcg_next(copy);
+                float choice_pdf = 1.0f;
+                while (mat->type == AKR_MAT_MIX) {  // Material::select_material, material.h:251-268
+                    const float frac = tex_eval(s, mat->fraction, tc).x;
+                    if (sel_u < frac) {
+                        sel_u = sel_u / frac;
+                        mat = &s.mats[mat->second];
+                        choice_pdf *= 1.0f / frac;
+                    } else {
+                        sel_u = (sel_u - frac) / (1.0f - frac);
+                        mat = &s.mats[mat->first];
+                        choice_pdf *= 1.0f / (1.0f - frac);
+                    }
+                }
+                Closure cl{CL_NONE, v3(0, 0, 0), 0.0f};
+                if (mat->type == AKR_MAT_DIFFUSE) {
+                    cl.kind = CL_DIFFUSE;
+                    cl.R = tex_eval(s, mat->color, tc);
+                } else if (mat->type == AKR_MAT_GLOSSY) {
+                    cl.kind = CL_GLOSSY;
+                    cl.R = tex_eval(s, mat->color, tc);
+                    float r = tex_eval(s, mat->roughness, tc).x;
+                    r *= r;
+                    cl.alpha = r;
+                }
+                const Frame frame = make_frame(ns);
+                const V2 bu = lcg_next2(seed);  // BSDFSampleContext(sampler.next2d(), wo)
+                if (cl.kind != CL_NONE) {
+                    V3 wi_l;
+                    float pdf = 0.0f;
+                    const V3 f = closure_sample(cl, bu, to_local(frame, wo), wi_l, pdf);
+                    const V3 wi = to_world(frame, wi_l);
+                    pdf *= choice_pdf;
+                    if (pdf != 0.0f) {
+                        const float cng = fabsf(dot(ng, wi));
+                        const V3 ev_beta = divs(muls(f, cng), pdf);
+                        // select_light(sampler.next2d()) — scene.h:79-90
+                        const V2 su = lcg_next2(seed);
+                        if (s.n_lights > 0) {
+                            int lo = 0, hi = s.n_lights + 1;  // upper_bound, distribution.h:32-44
+                            while (lo < hi) {
+                                const int m = (lo + hi) / 2;
+                                if (s.light_cdf[m] <= su.x) lo = m + 1; else hi = m;
+                            }
+                            int li = hi - 1;
+                            li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
+                            const float sel_pdf = s.light_func[li] / (s.light_func_int * (float)s.n_lights);
+                            const LightDev &lt = s.lights[li];
+                            const V2 lu = lcg_next2(seed);
+                            // AreaLight::sample (light.h:58-71)
+                            const float su0 = sqrtf(lu.x);
+                            const float b0 = 1 - su0, b1 = lu.y * su0;
+                            const V3 l0 = ld3(lt.v), l1 = ld3(lt.v + 3), l2 = ld3(lt.v + 6);
+                            const V3 lp = lerp3(l0, l1, l2, b0, b1);
+                            const V3 lx = cross(sub(l1, l0), sub(l2, l0));
+                            const V3 lng = normalize(lx);
+                            V3 lwi = sub(lp, p);
+                            const float dist_sqr = dot(lwi, lwi);
+                            lwi = divs(lwi, sqrtf(dist_sqr));
+                            const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]}, V2{lt.tc[4], lt.tc[5]}, b0, b1);
+                            const V3 Le = tex_eval(s, lt.color_tex, ltc);
+                            const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / (length(lx) * 0.5f);
+                            if (!(lpdf <= 0.0f)) {
+                                const float light_pdf = sel_pdf * lpdf;
+                                const V3 fe = closure_eval(cl, to_local(frame, wo), to_local(frame, lwi));
+                                const V3 fl = muls(mul(Le, fe), fabsf(dot(ns, lwi)));
+                                const V3 col = divs(mul(beta, fl), light_pdf);
+                                if (!is_black(col)) {
+                                    want_sh = true;
+                                    const V3 sd = neg(lwi);
+                                    s0 = make_float4(lp.x, lp.y, lp.z, kEps / fabsf(dot(lwi, lng)));
+                                    s1 = make_float4(sd.x, sd.y, sd.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
+                                    sc = make_float4(col.x, col.y, col.z, bitsf(slot));
+                                }
+                            }
+                        }
+                        const V3 nb = mul(beta, ev_beta);
+                        a.beta[slot] = make_float4(nb.x, nb.y, nb.z, 0.0f);
+                        want_ext = true;
+                        e0 = make_float4(p.x, p.y, p.z, kEps / cng);
+                        e1 = make_float4(wi.x, wi.y, wi.z, kInf);
+                    }
+                }
+                a.seed[slot] = seed;
+            }
+        }
+    }
+    const uint32_t pos = wave_append(want_ext, a.count_out);
+    if (want_ext) {
+        a.ray_out[2 * (size_t)pos] = e0;
+        a.ray_out[2 * (size_t)pos + 1] = e1;
+        a.slot_out[pos] = slot;
+    }
+    const uint32_t spos = wave_append(want_sh, a.shadow_count);
+    if (want_sh) {
+        a.shadow_ray[2 * (size_t)spos] = s0;
+        a.shadow_ray[2 * (size_t)spos + 1] = s1;
+        a.shadow_color[spos] = sc;
+    }
+}
+
+// ------------------------------------------------------------------------------------- splat
+__global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const float4 l = a.L[i];
+    float r = l.x, g = l.y, b = l.z;
+    if (a.ray_clamp > 0.0f) {  // clamp_zero + min (gpu/cuda/integrator.cpp:397-398)
+        r = isnan(r) ? 0.0f : rmax(0.0f, r);
+        g = isnan(g) ? 0.0f : rmax(0.0f, g);
+        b = isnan(b) ? 0.0f : rmax(0.0f, b);
+        r = rmin(r, a.ray_clamp);
+        g = rmin(g, a.ray_clamp);
+        b = rmin(b, a.ray_clamp);
+    }
+    float4 f = a.film[i];
+    f.x += r;
+    f.y += g;
+    f.z += b;
+    f.w += 1.0f;
+    a.film[i] = f;
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint32_t n, float *rad, float *w) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 f = film[i];
+    rad[3 * (size_t)i + 0] = f.x;
+    rad[3 * (size_t)i + 1] = f.y;
+    rad[3 * (size_t)i + 2] = f.z;
+    w[i] = f.w;
+}
+
+// ------------------------------------------------------------------------------------ launch
+static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
+
+template <int MODE>
+static void launch_trace_mode(bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
+    if (count) {
+        if (tight) hipLaunchKernelGGL((k_trace<MODE, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_trace<MODE, true, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    } else {
+        if (tight) hipLaunchKernelGGL((k_trace<MODE, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_trace<MODE, false, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    }
+}
+
+void launch_trace(int mode, bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
+    if (grid == 0) return;
+    if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST>(count, tight, a, grid, st);
+    else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY>(count, tight, a, grid, st);
+    else launch_trace_mode<TRACE_SHADOW>(count, tight, a, grid, st);
+}
+
+int trace_blocks_per_cu(int mode) {
+    int nb = 0;
+    hipError_t e;
+    if (mode == TRACE_CLOSEST)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true>, kBlock, 0);
+    else if (mode == TRACE_ANY)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true>, kBlock, 0);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true>, kBlock, 0);
+    if (e != hipSuccess || nb <= 0) nb = 1;
+    return nb;
+}
+
+void launch_raygen(const RaygenArgs &a, hipStream_t st) {
+    if (a.n == 0) return;
+    hipLaunchKernelGGL(k_raygen, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
+}
+void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items == 0) return;
+    hipLaunchKernelGGL(k_shade, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+}
+void launch_splat(const SplatArgs &a, hipStream_t st) {
+    if (a.n == 0) return;
+    hipLaunchKernelGGL(k_splat, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
+}
+void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_unpack_film, dim3(blocks_for(n)), dim3(kBlock), 0, st, film, n, rad, w);
+}
+
+}  // namespace akr

@@ -1,0 +1,193 @@
+"""Headline benchmark: Msamples/s of the wavefront path tracer on the synthetic 10M-triangle soup
+(BASELINE.json configs[2] / SURVEY.md §8d C3), 1920x1080, max_depth 5, tile-split across ranks.
+
+A step is one sample per pixel over the whole frame (2,073,600 path samples).  K steps are one
+render(spp=K) call per rank over that rank's tiles; the frame-end gather to rank 0 (RCCL via
+torch.distributed) is inside the timed region.  value = W*H*K / max-over-ranks time.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "akarirender-1_amd"))
+
+METRIC = "Msamples/sec (whole node), 10M-tri scene 1080p 1024spp, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic bytes per ray / AABB / triangle test
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def tiles_for_rank(W, H, tile, rank, world):
+    """Interleaved tile partition: tile k (row-major over the tile grid) -> rank k % world."""
+    out, k = [], 0
+    for y in range(0, H, tile):
+        for x in range(0, W, tile):
+            if k % world == rank:
+                out.append((x, y, min(W, x + tile), min(H, y + tile)))
+            k += 1
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tris", type=int, default=10_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--max-depth", type=int, default=5)
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--leaf", type=int, default=4)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-frac", type=int, default=64, help="CPU sample = every n-th tile of the frame")
+    ap.add_argument("--cpu-spp", type=int, default=1)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from akari_amd import capi, scene
+
+    W, H, K, Wm = args.width, args.height, args.steps, args.warmup
+    t0 = time.time()
+    sc = scene.soup_scene(n_tris=args.tris, resolution=(W, H))
+    cs = scene.compile_scene(sc)
+    t_gen = time.time() - t0
+    ctx = capi.HipContext(local)
+    info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, n_threads=min(16, os.cpu_count() or 1))
+    log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
+        f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
+
+    tiles = tiles_for_rank(W, H, args.tile, rank, world)
+    npix = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles)
+    maxpix = max(sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles_for_rank(W, H, args.tile, r, world))
+                 for r in range(world))
+    film = torch.zeros(maxpix * 4, device=dev)          # [radiance rgb (packed) | weight]
+    rad, wgt = film[:maxpix * 3], film[maxpix * 3:]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    # warmup (also JIT/cache warm)
+    if Wm > 0:
+        ctx.render_device(Wm, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+
+    # untimed counting pass: traversal tests of one sample pass (algorithmic bytes)
+    ctx.set_option("count_tests", 1)
+    ctx.reset_stats()
+    ctx.set_option("stats", 1)
+    ctx.render_device(1, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    counts = ctx.trace_counts()
+    cstats = ctx.kernel_stats()
+    ctx.set_option("count_tests", 0)
+    ctx.reset_stats()
+
+    # timed region
+    gathered = None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    ctx.render_device(K, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+    if world > 1:
+        gathered = torch.empty(world * film.numel(), device=dev)
+        dist.all_gather_into_tensor(gathered, film)     # frame-end gather over RCCL
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kstats = ctx.kernel_stats()
+
+    # sanity: every pixel of this rank got K samples
+    assert int(wgt[:npix].min().item()) == K and int(wgt[:npix].max().item()) == K
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    samples = W * H * K
+    value = samples / elapsed / 1e6
+    # roofline of the dominant kernel (closest-hit traversal)
+    cl = counts["per_mode"]["closest"]
+    n_cl_launch = cstats.get("trace_closest", {}).get("launches", 0) or 1
+    bytes_per_launch = (RAY_BYTES * cl["rays"] + BOX_BYTES * cl["box_tests"] + TRI_BYTES * cl["tri_tests"]) / n_cl_launch
+    kc = kstats["trace_closest"]
+    avg_ms = kc["total_ms"] / kc["launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    sh = counts["per_mode"]["shadow"]
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "trace_closest", "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
+                "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
+                            "tri_tests": cl["tri_tests"] / max(1, cl["rays"])},
+                "shadow_per_ray": {"box_tests": sh["box_tests"] / max(1, sh["rays"]),
+                                   "tri_tests": sh["tri_tests"] / max(1, sh["rays"])}}
+
+    cpu = None
+    if args.cpu_baseline and world == 1:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import py_oracle
+        nodes, tris = ctx.accel_export()
+        orc = py_oracle.OracleScene(cs, nodes, tris, capi)
+        ctiles = tiles_for_rank(W, H, args.tile, 0, args.cpu_frac)
+        cpx = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in ctiles)
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        # the reference CPU path's traversal (exact intersectAABB), and the same port with the tight cull
+        tc = time.perf_counter()
+        orc.render(args.cpu_spp, args.max_depth, tiles=ctiles, n_threads=threads, exact_cull=True)
+        dt = time.perf_counter() - tc
+        tc = time.perf_counter()
+        orc.render(args.cpu_spp, args.max_depth, tiles=ctiles, n_threads=threads, exact_cull=False)
+        dt_tight = time.perf_counter() - tc
+        cpu = {"value": round(cpx * args.cpu_spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+               "kind": "port",
+               "sample": f"every {args.cpu_frac}th {args.tile}x{args.tile} tile of the same frame ({cpx} px) x "
+                         f"{args.cpu_spp} spp, same scene and BVH, reference intersectAABB, {dt:.1f} s",
+               "value_tight_cull": round(cpx * args.cpu_spp / dt_tight / 1e6, 4)}
+
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
+        "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)", "triangles": cs.n_tris,
+                   "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
+                   "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf},
+        "roofline": roofline, "cpu_baseline": cpu,
+        "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
+                    for k, v in kstats.items()},
+        "bvh": {"nodes": info.n_nodes, "depth": info.max_depth, "build_s": round(info.build_ms / 1e3, 2)},
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,54 @@
+/*
+ * akr_bvh_format.h — in-memory layout of the acceleration structure produced by
+ * akr_hip_build_accel (data format only; no algorithms live here).
+ *
+ * BVH2 with both child boxes stored in the parent ("child boxes in parent"): one 64-byte node
+ * fetch (one half of a 128-byte HBM line) serves the two AABB tests of a traversal step, and a
+ * culled child is never fetched.  This replaces the reference's per-node 64-byte BVHNode
+ * (src/akari/kernel/bvh-accelerator.h:34-57) whose box is tested when the node is popped; the
+ * traversal order (near child = left iff ray.d[axis] > 0, bvh-accelerator.h:43-56, 508-514) and
+ * the cull rule (entry t < 0 or entry t > best t, :500) are kept, see DESIGN.md §3.
+ *
+ * Node 0 is a virtual root: child[0] is the real root (or a leaf), child[1] is EMPTY, so the
+ * root box is tested exactly once like the reference's first intersectAABB.
+ */
+#ifndef AKR_BVH_FORMAT_H
+#define AKR_BVH_FORMAT_H
+#include <stdint.h>
+
+#define AKR_CHILD_EMPTY 0xFFFFFFFFu
+#define AKR_CHILD_LEAF 0x80000000u   /* leaf reference: LEAF | (first << 3) | (count - 1) */
+#define AKR_LEAF_MAX 8
+#define AKR_BVH_MAX_DEPTH 64
+
+#if defined(__HIPCC__)
+#define AKR_HD __host__ __device__
+#else
+#define AKR_HD
+#endif
+
+typedef struct akr_bvh_node {
+    float bxy0[4]; /* child 0: lo.x, hi.x, lo.y, hi.y */
+    float bxy1[4]; /* child 1: lo.x, hi.x, lo.y, hi.y */
+    float bz[4];   /* child 0: lo.z, hi.z; child 1: lo.z, hi.z */
+    uint32_t child[2];
+    uint32_t axis; /* split axis of this node (0, 1, 2) */
+    uint32_t _pad;
+} akr_bvh_node;
+
+/* Leaf-ordered triangle: v0, e1 = v1 - v0, e2 = v2 - v0 (computed in f32 on the host, the same
+ * rounding as the reference's in-loop subtraction, instance.h:49-50), global triangle id. */
+typedef struct akr_bvh_tri {
+    float v0[3];
+    uint32_t gid;
+    float e1[3];
+    uint32_t _pad0;
+    float e2[3];
+    uint32_t _pad1;
+} akr_bvh_tri;
+
+static inline AKR_HD int akr_child_is_leaf(uint32_t c) { return c != AKR_CHILD_EMPTY && (c & AKR_CHILD_LEAF); }
+static inline AKR_HD uint32_t akr_leaf_first(uint32_t c) { return (c & 0x7FFFFFFFu) >> 3; }
+static inline AKR_HD uint32_t akr_leaf_count(uint32_t c) { return (c & 7u) + 1u; }
+
+#endif

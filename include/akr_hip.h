@@ -1,0 +1,214 @@
+/*
+ * akr_hip.h — C-ABI drop-in boundary of the MI355X (gfx950) ray-scene intersection and
+ * unidirectional path-tracing backend for AkariRender.
+ *
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.  Every export
+ * returns an int status (0 = ok) and never throws or aborts across the ABI; the message of the
+ * last failure on a context is available from akr_hip_last_error().  The C++ host adapter
+ * (akarirender-1_amd/csrc/akari_hip.hpp) turns a non-zero status into std::runtime_error, the
+ * reference's AKR_ASSERT_THROW convention (src/akari/common/panic.h:52-57).
+ *
+ * What each entry point replaces in the reference (paths relative to the reference root):
+ *
+ *  akr_hip_upload_mesh       MeshInstance<C> views built by AkariMesh::compile
+ *                            (src/akari/core/nodes/mesh.cpp:47-61; layout kernel/instance.h:30-35)
+ *  akr_hip_upload_textures   ConstantTexture / ImageTexture  (src/akari/kernel/texture.h:30-66)
+ *  akr_hip_upload_materials  Material<C> closed Variant     (src/akari/kernel/material.h:205-298)
+ *  akr_hip_upload_lights     AreaLight list + Distribution1D built in SceneNode::compile
+ *                            (src/akari/core/nodes/scene.cpp:51-92; common/distribution.h:46-102)
+ *  akr_hip_build_accel       BVHAccelerator<C>::build / Scene<C>::commit
+ *                            (src/akari/kernel/bvh-accelerator.h:673-678; kernel/scene.cpp:64-81)
+ *  akr_hip_trace (any_hit=0) BVHAccelerator<C>::intersect  (bvh-accelerator.h:679-681, 488-518)
+ *  akr_hip_trace (any_hit=1) BVHAccelerator<C>::occlude    (bvh-accelerator.h:682, 519-547)
+ *  akr_hip_set_camera        PerspectiveCameraNode::compile + PerspectiveCamera::preprocess
+ *                            (src/akari/core/nodes/camera.cpp:26-52; kernel/camera.h:45-59)
+ *  akr_hip_render            gpu::PathTracer<C>::render / cpu::PathTracer<C>::render
+ *                            (kernel/integrators/gpu/cuda/integrator.cpp:137-424,
+ *                             kernel/integrators/cpu/integrator.cpp:89-142), called from
+ *                             SceneNode::render (src/akari/core/nodes/scene.cpp:137-150)
+ *  akr_hip_kernel_stats      print_kernel_stats (src/akari/kernel/cuda/launch.cpp:92-118)
+ *
+ * Semantics are those of the reference CPU path (no radiance clamp unless ray_clamp > 0,
+ * max_depth from the parameters, NEE only, LCG sampler seeded x + y*W per pixel).
+ */
+#ifndef AKR_HIP_H
+#define AKR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AKR_HIP_API_VERSION 1
+
+typedef struct akr_hip_ctx akr_hip_ctx;
+
+/* Ray<C> (common/math.h:183-199): origin, tmin, direction, tmax.  32 bytes. */
+typedef struct akr_ray {
+    float o[3];
+    float tmin;
+    float d[3];
+    float tmax;
+} akr_ray;
+
+/* Intersection<C> (kernel/scene.h:40-49).  Miss: t = +inf, geom_id = prim_id = -1. 32 bytes. */
+typedef struct akr_hit {
+    float t;
+    float u, v;        /* barycentrics (b1, b2) of the Moller-Trumbore test, instance.h:57-68 */
+    int32_t geom_id;   /* index of the mesh in upload order */
+    int32_t prim_id;   /* triangle index inside that mesh */
+    int32_t _pad[3];
+} akr_hit;
+
+enum { AKR_TEX_CONSTANT = 0, AKR_TEX_IMAGE = 1 };
+typedef struct akr_texture {
+    int32_t type;      /* AKR_TEX_CONSTANT: value[] used; AKR_TEX_IMAGE: image index */
+    float value[3];
+    int32_t image;
+    int32_t _pad[3];
+} akr_texture;
+
+enum { AKR_MAT_DIFFUSE = 0, AKR_MAT_GLOSSY = 1, AKR_MAT_EMISSIVE = 2, AKR_MAT_MIX = 3 };
+typedef struct akr_material {
+    int32_t type;
+    int32_t color;      /* texture index: Diffuse/Glossy/Emissive colour */
+    int32_t roughness;  /* texture index: Glossy roughness (x channel, squared -> alpha) */
+    int32_t fraction;   /* texture index: Mix fraction (x channel) */
+    int32_t first;      /* material index: Mix material_A */
+    int32_t second;     /* material index: Mix material_B */
+    int32_t double_sided; /* Emissive */
+    int32_t _pad;
+} akr_material;
+
+/* One emissive triangle (AreaLight, kernel/light.h:47-71). */
+typedef struct akr_area_light {
+    int32_t geom_id;
+    int32_t prim_id;
+} akr_area_light;
+
+/* PerspectiveCameraNode fields (core/nodes/camera.cpp:26-52). */
+typedef struct akr_camera {
+    float position[3];
+    float rotation_deg[3];
+    double fov_deg;
+    int32_t resolution[2];
+    int32_t _pad[2];
+} akr_camera;
+
+/* Path node fields (core/nodes/integrator.cpp:50-84).  ray_clamp <= 0 disables the clamp
+ * (reference CPU semantics); > 0 clamps each sample to [0, ray_clamp] (GPU semantics).
+ * flags: AKR_PT_EXACT_CULL = traverse with the reference's intersectAABB bit for bit (it keeps
+ * boxes that lie behind the ray origin); default is the standard slab test, same hits. */
+#define AKR_PT_EXACT_CULL 1
+typedef struct akr_pt_params {
+    int32_t spp;
+    int32_t max_depth;
+    float ray_clamp;
+    int32_t flags;
+} akr_pt_params;
+
+/* Pixel rectangle [x0, x1) x [y0, y1). */
+typedef struct akr_rect {
+    int32_t x0, y0, x1, y1;
+} akr_rect;
+
+typedef struct akr_build_params {
+    int32_t max_leaf_size;  /* <= 8 */
+    int32_t n_bins;         /* SAH bins per axis (reference: 32, bvh-accelerator.h:104) */
+    float traversal_cost;
+    float intersect_cost;
+    int32_t n_threads;      /* 0 = hardware concurrency */
+    int32_t _pad[3];
+} akr_build_params;
+
+typedef struct akr_accel_info {
+    uint64_t n_nodes;       /* 64-byte BVH2 nodes, node 0 is the virtual root */
+    uint64_t n_tris;        /* 48-byte leaf-ordered triangle records */
+    int32_t max_depth;
+    int32_t max_leaf;
+    double build_ms;
+    double sah_cost;
+} akr_accel_info;
+
+typedef struct akr_kernel_stat {
+    char name[48];
+    uint64_t launches;
+    double total_ms;
+    double min_ms;
+    double max_ms;
+} akr_kernel_stat;
+
+/* Traversal counters (filled when option "count_tests" is 1). */
+typedef struct akr_trace_counts {
+    uint64_t rays;
+    uint64_t box_tests;
+    uint64_t tri_tests;
+    uint64_t closest_rays;
+    uint64_t shadow_rays;
+    uint64_t per_mode[3][3]; /* [closest, any-hit, shadow] x [rays, box_tests, tri_tests] */
+} akr_trace_counts;
+
+int akr_hip_api_version(void);
+int akr_hip_device_count(int *n);
+
+int akr_hip_create(int device, akr_hip_ctx **out);
+int akr_hip_destroy(akr_hip_ctx *ctx);
+const char *akr_hip_last_error(const akr_hip_ctx *ctx);
+/* Options: "stats" (per-kernel HIP-event timing on/off), "count_tests" (traversal counters),
+ * "stack_lds" (read-only). */
+int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value);
+
+int akr_hip_upload_mesh(akr_hip_ctx *ctx, const float *vertices, uint64_t n_vertices,
+                        const int32_t *indices, const float *normals, const float *texcoords,
+                        const int32_t *material_indices, uint64_t n_triangles,
+                        const int32_t *material_slots, int32_t n_slots, int32_t *geom_id);
+int akr_hip_upload_images(akr_hip_ctx *ctx, const float *rgba, const int32_t *widths,
+                          const int32_t *heights, int32_t n_images);
+int akr_hip_upload_textures(akr_hip_ctx *ctx, const akr_texture *textures, int32_t n);
+int akr_hip_upload_materials(akr_hip_ctx *ctx, const akr_material *materials, int32_t n);
+int akr_hip_upload_lights(akr_hip_ctx *ctx, const akr_area_light *lights, int32_t n,
+                          const float *power);
+int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params);
+int akr_hip_accel_info(akr_hip_ctx *ctx, akr_accel_info *info);
+int akr_hip_accel_export(akr_hip_ctx *ctx, void *nodes, uint64_t node_bytes, void *tris,
+                         uint64_t tri_bytes);
+int akr_hip_set_camera(akr_hip_ctx *ctx, const akr_camera *camera);
+
+/* Batched trace, host buffers in and out, synchronous. */
+int akr_hip_trace(akr_hip_ctx *ctx, const akr_ray *rays, uint64_t n, akr_hit *hits, int any_hit);
+/* Batched trace on device buffers (akr_ray[n] -> akr_hit[n]) on `stream` (hipStream_t, may be 0). */
+int akr_hip_trace_device(akr_hip_ctx *ctx, const void *d_rays, uint64_t n, void *d_hits,
+                         int any_hit, void *stream);
+
+/* Render the pixels of `tiles` (clipped to the camera resolution) and ACCUMULATE into host
+ * full-frame buffers radiance[W*H*3] (sum of L) and weight[W*H] (sample count), the reference
+ * Film's Pixel{radiance, weight} (core/film.h:31-35).  Synchronous. */
+int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles,
+                   int32_t n_tiles, float *radiance, float *weight);
+/* Same, but writes (overwrites) device buffers in packed tile order: pixel k of the tile list
+ * (tiles in order, row-major inside a tile) -> radiance[3k..3k+2], weight[k].  Returns the
+ * pixel count in *n_pixels.  Asynchronous on `stream`. */
+int akr_hip_render_device(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles,
+                          int32_t n_tiles, float *d_radiance, float *d_weight, void *stream,
+                          uint64_t *n_pixels);
+
+/* Host-only BVH build (no device needed): the same builder akr_hip_build_accel runs, for tools
+ * and CPU-side checks.  Arrays are owned by the handle; free with akr_bvh_host_free. */
+typedef struct akr_bvh_host akr_bvh_host;
+int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t *indices,
+                       uint64_t n_triangles, const akr_build_params *params, akr_bvh_host **out,
+                       akr_accel_info *info);
+const void *akr_bvh_host_nodes(const akr_bvh_host *h);
+const void *akr_bvh_host_tris(const akr_bvh_host *h);
+void akr_bvh_host_free(akr_bvh_host *h);
+
+int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n);
+int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
+int akr_hip_reset_stats(akr_hip_ctx *ctx);
+int akr_hip_synchronize(akr_hip_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AKR_HIP_H */

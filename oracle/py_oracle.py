@@ -1,0 +1,213 @@
+"""ctypes binding of the CPU restatement (oracle/akr_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the cpu_baseline leg of
+bench.py, as the checker.  Never imported by the product package (akarirender-1_amd/akari_amd).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "libakr_oracle.so"
+
+_P = C.c_void_p
+
+
+class OrcScene(C.Structure):
+    _fields_ = [
+        ("vertices", _P), ("n_vertices", C.c_uint64), ("indices", _P), ("normals", _P), ("texcoords", _P),
+        ("matid", _P), ("n_tris", C.c_uint64), ("materials", _P), ("n_materials", C.c_int32), ("textures", _P),
+        ("n_textures", C.c_int32), ("images", _P), ("image_offset", _P), ("image_w", _P), ("image_h", _P),
+        ("n_images", C.c_int32), ("light_gid", _P), ("light_power", _P), ("n_lights", C.c_int32), ("nodes", _P),
+        ("n_nodes", C.c_uint64), ("tris", _P), ("n_bvh_tris", C.c_uint64),
+        ("camera", C.c_byte * 48),
+    ]
+
+
+class OrcStats(C.Structure):
+    _fields_ = [("camera_rays", C.c_uint64), ("extension_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("box_tests", C.c_uint64), ("tri_tests", C.c_uint64)]
+
+
+ORC_HIT = np.dtype([("t", np.float32), ("u", np.float32), ("v", np.float32), ("gid", np.uint32)])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        l = C.CDLL(str(LIB))
+        l.orc_lcg.restype = C.c_uint32
+        l.orc_lcg.argtypes = [C.c_uint32, C.c_int32, _P]
+        l.orc_pcg.restype = None
+        l.orc_pcg.argtypes = [C.c_uint64, C.c_int64, _P]
+        l.orc_camera_ray.argtypes = [_P, C.c_int32, C.c_int32, C.POINTER(C.c_uint32), _P]
+        l.orc_camera_matrices.argtypes = [_P, _P, _P]
+        l.orc_camera_matrices.restype = None
+        l.orc_distribution_sample.argtypes = [_P, C.c_int32, _P, C.c_int32, _P, _P]
+        l.orc_distribution_sample.restype = None
+        l.orc_frame_roundtrip.argtypes = [_P, _P, _P, _P]
+        l.orc_frame_roundtrip.restype = None
+        l.orc_cosine_hemisphere.argtypes = [_P, C.c_int32, _P]
+        l.orc_cosine_hemisphere.restype = None
+        l.orc_trace.argtypes = [C.POINTER(OrcScene), _P, C.c_uint64, _P, C.c_int, C.c_int32, C.c_int32,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        l.orc_trace_brute.argtypes = [C.POINTER(OrcScene), _P, C.c_uint64, _P, C.c_int, C.c_int32]
+        l.orc_render.argtypes = [C.POINTER(OrcScene), _P, _P, C.c_int32, _P, _P, C.c_int32, C.POINTER(OrcStats)]
+        _lib = l
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(_P) if a is not None else None
+
+
+def lcg(seed: int, n: int):
+    out = np.zeros(n, np.float32)
+    s = lib().orc_lcg(seed & 0xFFFFFFFF, n, _p(out))
+    return out, s
+
+
+def pcg(seed: int, n: int):
+    out = np.zeros(n, np.float32)
+    lib().orc_pcg(seed, n, _p(out))
+    return out
+
+
+def _camera_bytes(cam, capi):
+    c = capi.Camera((C.c_float * 3)(*cam.position), (C.c_float * 3)(*cam.rotation), float(cam.fov),
+                    (C.c_int32 * 2)(*cam.resolution))
+    return c
+
+
+def camera_ray(cam, capi, x, y, seed):
+    c = _camera_bytes(cam, capi)
+    s = C.c_uint32(seed & 0xFFFFFFFF)
+    out = np.zeros(1, capi.RAY_DTYPE)
+    lib().orc_camera_ray(C.byref(c), x, y, C.byref(s), _p(out))
+    return out[0], s.value
+
+
+def camera_matrices(cam, capi):
+    c = _camera_bytes(cam, capi)
+    r2c = np.zeros(16, np.float32)
+    c2w = np.zeros(16, np.float32)
+    lib().orc_camera_matrices(C.byref(c), _p(r2c), _p(c2w))
+    return r2c.reshape(4, 4), c2w.reshape(4, 4)
+
+
+def distribution_sample(func, u):
+    func = np.ascontiguousarray(func, np.float32)
+    u = np.ascontiguousarray(u, np.float32)
+    idx = np.zeros(u.size, np.int32)
+    pdf = np.zeros(u.size, np.float32)
+    lib().orc_distribution_sample(_p(func), func.size, _p(u), u.size, _p(idx), _p(pdf))
+    return idx, pdf
+
+
+def frame_roundtrip(n, w):
+    n = np.ascontiguousarray(n, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    a = np.zeros(3, np.float32)
+    b = np.zeros(3, np.float32)
+    lib().orc_frame_roundtrip(_p(n), _p(w), _p(a), _p(b))
+    return a, b
+
+
+def cosine_hemisphere(u2):
+    u2 = np.ascontiguousarray(u2, np.float32).reshape(-1, 2)
+    out = np.zeros((u2.shape[0], 3), np.float32)
+    lib().orc_cosine_hemisphere(_p(u2), u2.shape[0], _p(out))
+    return out
+
+
+class OracleScene:
+    """Holds the arrays an orc_scene points into (CompiledScene + BVH arrays)."""
+
+    def __init__(self, cs, nodes, tris, capi):
+        self.capi = capi
+        self.keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(a, dt)
+            self.keep.append(a)
+            return a
+
+        v = arr(cs.vertices, np.float32)
+        i = arr(cs.indices, np.int32)
+        n = arr(cs.normals, np.float32)
+        t = arr(cs.texcoords, np.float32)
+        m = arr(cs.matid, np.int32)
+        mats = (capi.Material * max(1, len(cs.materials)))(*cs.materials)
+        texs = (capi.Texture * max(1, len(cs.textures)))(*cs.textures)
+        self.keep += [mats, texs]
+        if cs.images:
+            imgs = arr(np.concatenate([im.reshape(-1) for im in cs.images]), np.float32)
+            offs = np.cumsum([0] + [im.size for im in cs.images[:-1]]).astype(np.int64)
+            offs = arr(offs, np.int64)
+            iw = arr([im.shape[1] for im in cs.images], np.int32)
+            ih = arr([im.shape[0] for im in cs.images], np.int32)
+        else:
+            imgs = offs = iw = ih = None
+        lg = arr(cs.light_gid, np.uint32)
+        pw = arr(cs.power, np.float32)
+        nd = arr(nodes, nodes.dtype)
+        tr = arr(tris, tris.dtype)
+        s = OrcScene()
+        s.vertices, s.n_vertices = _p(v), v.shape[0]
+        s.indices, s.normals, s.texcoords, s.matid, s.n_tris = _p(i), _p(n), _p(t), _p(m), m.shape[0]
+        s.materials, s.n_materials = C.cast(mats, _P), len(cs.materials)
+        s.textures, s.n_textures = C.cast(texs, _P), len(cs.textures)
+        s.images, s.image_offset, s.image_w, s.image_h = _p(imgs), _p(offs), _p(iw), _p(ih)
+        s.n_images = len(cs.images)
+        s.light_gid, s.light_power, s.n_lights = _p(lg), _p(pw), len(cs.lights)
+        s.nodes, s.n_nodes, s.tris, s.n_bvh_tris = _p(nd), nd.shape[0], _p(tr), tr.shape[0]
+        cam = _camera_bytes(cs.camera, capi)
+        C.memmove(C.addressof(s) + OrcScene.camera.offset, C.addressof(cam), C.sizeof(cam))
+        self.s = s
+        self.width, self.height = int(cs.camera.resolution[0]), int(cs.camera.resolution[1])
+
+    def trace(self, rays, any_hit=False, n_threads=0, exact_cull=False):
+        rays = np.ascontiguousarray(rays, self.capi.RAY_DTYPE)
+        hits = np.zeros(rays.shape[0], ORC_HIT)
+        nb, nt = C.c_uint64(0), C.c_uint64(0)
+        lib().orc_trace(C.byref(self.s), _p(rays), rays.shape[0], _p(hits), int(any_hit), int(not exact_cull),
+                        n_threads, C.byref(nb),
+                        C.byref(nt))
+        return hits, nb.value, nt.value
+
+    def trace_brute(self, rays, any_hit=False, n_threads=0):
+        rays = np.ascontiguousarray(rays, self.capi.RAY_DTYPE)
+        hits = np.zeros(rays.shape[0], ORC_HIT)
+        lib().orc_trace_brute(C.byref(self.s), _p(rays), rays.shape[0], _p(hits), int(any_hit), n_threads)
+        return hits
+
+    def render(self, spp, max_depth, tiles=None, ray_clamp=0.0, n_threads=0, radiance=None, weight=None,
+               exact_cull=False):
+        W, H = self.width, self.height
+        if tiles is None:
+            tiles = [(0, 0, W, H)]
+        if radiance is None:
+            radiance = np.zeros((H, W, 3), np.float32)
+        if weight is None:
+            weight = np.zeros((H, W), np.float32)
+        p = self.capi.PtParams(int(spp), int(max_depth), float(ray_clamp), 1 if exact_cull else 0)
+        rects = (self.capi.Rect * max(1, len(tiles)))(*[self.capi.Rect(*t) for t in tiles])
+        st = OrcStats()
+        lib().orc_render(C.byref(self.s), C.byref(p), C.cast(rects, _P), len(tiles), _p(radiance), _p(weight),
+                         n_threads, C.byref(st))
+        stats = dict(camera_rays=st.camera_rays, extension_rays=st.extension_rays, shadow_rays=st.shadow_rays,
+                     box_tests=st.box_tests, tri_tests=st.tri_tests)
+        return radiance, weight, stats

@@ -1,0 +1,62 @@
+"""Shared test inputs: seeded ray batches and small scenes."""
+import numpy as np
+
+from akari_amd import capi, scene
+
+
+def random_rays(n, seed, lo, hi, tmin=1e-3, tmax=np.inf):
+    """Origins uniform in the box [lo, hi]^3, directions uniform on the sphere (normalised in f32)."""
+    rng = np.random.default_rng(seed)
+    r = np.zeros(n, capi.RAY_DTYPE)
+    r["o"] = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    r["d"] = d
+    r["tmin"] = np.float32(tmin)
+    r["tmax"] = np.float32(tmax)
+    return r
+
+
+def edge_rays(center=(0.0, 0.0, 0.0)):
+    """Axis-aligned directions (zero components -> inf/NaN slabs), degenerate intervals, +-0."""
+    c = np.asarray(center, np.float32)
+    dirs = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1), (-0.0, -1, 0.0),
+            (0.5, 0.5, 0.0), (0, 0.5, -0.5), (1e-30, 1, 0)]
+    rays = []
+    for d in dirs:
+        d = np.asarray(d, np.float32)
+        d = d / np.float32(np.sqrt(np.float32(np.dot(d, d))))
+        for tmin, tmax in ((1e-3, np.inf), (0.0, np.inf), (1e-3, 1e-3), (5.0, 1.0), (1e-3, 0.5)):
+            r = np.zeros(1, capi.RAY_DTYPE)
+            r["o"], r["d"], r["tmin"], r["tmax"] = c, d, tmin, tmax
+            rays.append(r)
+    return np.concatenate(rays)
+
+
+def cornell(resolution=(64, 64)):
+    from conftest import CORNELL_MESH
+    return scene.cornell_scene(CORNELL_MESH, resolution=resolution)
+
+
+def small_soup(n_tris=20000, resolution=(96, 54), seed=42):
+    return scene.soup_scene(n_tris=n_tris, resolution=resolution, seed=seed)
+
+
+def mixed_scene(resolution=(48, 48)):
+    """Cornell geometry with Glossy / Mix materials and a two-sided emitter (BSDF coverage)."""
+    sc = cornell(resolution)
+    m = sc.shapes[0]
+    ct = scene.ConstantTexture
+    glossy = scene.GlossyMaterial(ct([0.9, 0.8, 0.7]), ct([0.4, 0.4, 0.4]))
+    mix = scene.MixMaterial(ct([0.3, 0.3, 0.3]), scene.DiffuseMaterial(ct([0.2, 0.7, 0.2])), glossy)
+    m.materials[5] = glossy       # short box
+    m.materials[6] = mix          # tall box
+    m.materials[7] = scene.EmissiveMaterial(ct([17.0, 12.0, 4.0]), double_sided=True)
+    return sc
+
+
+def hits_to_gid(hits, mesh_base):
+    gid = np.full(hits.shape[0], 0xFFFFFFFF, np.uint32)
+    ok = hits["geom_id"] >= 0
+    gid[ok] = mesh_base[hits["geom_id"][ok]] + hits["prim_id"][ok].astype(np.uint32)
+    return gid

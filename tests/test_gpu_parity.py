@@ -1,0 +1,170 @@
+"""HIP path (libakr_hip.so through the C-ABI) against the CPU restatement, on device 0.
+
+Bar: bit-exact.  The oracle traverses the same BVH arrays with the reference's own algorithm
+(bvh-accelerator.h:488-547), so hit ids, t and barycentrics must match exactly; renders must
+match exactly because every f32 operation is kept in the reference's order on both sides
+(DESIGN.md §4).  Tolerances appear only where the reference itself is builder-dependent.
+"""
+import numpy as np
+import pytest
+
+import py_oracle
+from akari_amd import capi, scene
+from helpers import cornell, edge_rays, hits_to_gid, mixed_scene, random_rays, small_soup
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(ctx, sc, **kw):
+    cs = scene.compile_scene(sc)
+    scene.upload_scene(ctx, cs, **kw)
+    nodes, tris = ctx.accel_export()
+    return cs, py_oracle.OracleScene(cs, nodes, tris, capi)
+
+
+def _check_trace(ctx, orc, cs, rays, any_hit, exact=False):
+    ctx.set_option("exact_cull", int(exact))
+    gh = ctx.trace(rays, any_hit=any_hit)
+    oh, _, _ = orc.trace(rays, any_hit=any_hit, exact_cull=exact)
+    ggid = hits_to_gid(gh, cs.mesh_base)
+    assert np.array_equal(ggid, oh["gid"]), f"{np.count_nonzero(ggid != oh['gid'])} hit ids differ"
+    hit = oh["gid"] != 0xFFFFFFFF
+    assert np.array_equal(gh["t"][hit], oh["t"][hit])
+    assert np.all(np.isinf(gh["t"][~hit]))
+    if not any_hit:
+        assert np.array_equal(gh["u"][hit], oh["u"][hit]) and np.array_equal(gh["v"][hit], oh["v"][hit])
+    assert np.all(gh["geom_id"][~hit] == -1) and np.all(gh["prim_id"][~hit] == -1)
+    return gh, oh
+
+
+@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_trace_cornell(hip_ctx_factory, any_hit, exact):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell())
+        rays = random_rays(1 << 16, 1, -0.9, 0.9)
+        rays["o"][:, 1] += 1.0          # the box spans y in [0, 2]
+        _check_trace(ctx, orc, cs, rays, any_hit, exact)
+        _check_trace(ctx, orc, cs, edge_rays((0.0, 1.0, 0.0)), any_hit, exact)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_trace_soup(hip_ctx_factory, any_hit, exact):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(100_000))
+        rays = random_rays(1 << 17, 2, -1.2, 1.2)
+        _check_trace(ctx, orc, cs, rays, any_hit, exact)
+        _check_trace(ctx, orc, cs, edge_rays(), any_hit, exact)
+
+
+def test_tight_cull_same_hits_as_reference_cull(hip_ctx_factory):
+    """The default slab test (behind-origin boxes culled) returns the reference cull's hits."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(100_000))
+        rays = random_rays(1 << 17, 6, -1.2, 1.2)
+        ctx.set_option("exact_cull", 0)
+        a = ctx.trace(rays)
+        ctx.set_option("exact_cull", 1)
+        b = ctx.trace(rays)
+        assert (hits_to_gid(a, cs.mesh_base) == hits_to_gid(b, cs.mesh_base)).mean() >= 0.9999
+        assert np.array_equal(a["t"], b["t"])
+
+
+def test_trace_builder_independent(hip_ctx_factory):
+    """Closest hits agree with a BVH-free brute force (builder independence, >= 99.99 %)."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(20_000))
+        rays = random_rays(1 << 13, 3, -1.1, 1.1)
+        gh = ctx.trace(rays)
+        bh = orc.trace_brute(rays)
+        same = hits_to_gid(gh, cs.mesh_base) == bh["gid"]
+        assert same.mean() >= 0.9999
+        both = same & (bh["gid"] != 0xFFFFFFFF)
+        assert np.array_equal(gh["t"][both], bh["t"][both])
+
+
+@pytest.mark.parametrize("leaf", [1, 2, 8])
+def test_trace_leaf_sizes(hip_ctx_factory, leaf):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(30_000), max_leaf_size=leaf)
+        assert ctx.accel_info().max_leaf <= leaf
+        _check_trace(ctx, orc, cs, random_rays(1 << 14, 4, -1.1, 1.1), False)
+
+
+def test_trace_empty_and_device_batch(hip_ctx_factory):
+    torch = pytest.importorskip("torch")
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell())
+        assert ctx.trace(np.zeros(0, capi.RAY_DTYPE)).shape == (0,)
+        rays = random_rays(4096, 5, -0.9, 0.9)
+        rays["o"][:, 1] += 1.0
+        d_r = torch.from_numpy(rays.view(np.uint8).copy()).to("cuda:0")
+        d_h = torch.zeros(4096 * 32, dtype=torch.uint8, device="cuda:0")
+        ctx.trace_device(d_r.data_ptr(), 4096, d_h.data_ptr(), any_hit=False)
+        ctx.synchronize()
+        gh = d_h.cpu().numpy().view(capi.HIT_DTYPE)
+        oh, _, _ = orc.trace(rays)
+        assert np.array_equal(hits_to_gid(gh, cs.mesh_base), oh["gid"])
+
+
+def _check_render(ctx, orc, spp, depth, tiles, W, H, clamp=0.0, exact=False):
+    rad, w = ctx.render(spp, depth, tiles, W, H, ray_clamp=clamp, exact_cull=exact)
+    orad, ow, _ = orc.render(spp, depth, tiles=tiles, ray_clamp=clamp, exact_cull=exact)
+    assert np.array_equal(w, ow)
+    bad = rad != orad
+    assert not bad.any(), f"{bad.sum()} radiance values differ, max {np.abs(rad - orad).max()}"
+    return rad, w
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_render_cornell_bit_exact(hip_ctx_factory, exact):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((64, 64)))
+        rad, w = _check_render(ctx, orc, 16, 5, [(0, 0, 64, 64)], 64, 64, exact=exact)
+        assert np.all(w == 16) and rad.mean() > 0
+
+
+def test_render_tiles_depths_clamp(hip_ctx_factory):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((40, 24)))
+        tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]   # ragged, clipped, empty
+        for depth in (0, 1, 2, 5):
+            _check_render(ctx, orc, 3, depth, tiles, 40, 24)
+        _check_render(ctx, orc, 4, 5, tiles, 40, 24, clamp=10.0)
+        rad, w = ctx.render(0, 5, tiles, 40, 24)
+        assert not w.any() and not rad.any()
+        rad, w = ctx.render(2, 5, [], 40, 24)
+        assert not w.any()
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_render_soup_bit_exact(hip_ctx_factory, exact):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(50_000, (64, 36)))
+        _check_render(ctx, orc, 4, 5, [(0, 0, 64, 36)], 64, 36, exact=exact)
+
+
+def test_render_glossy_mix_bit_exact(hip_ctx_factory):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, mixed_scene((48, 48)))
+        _check_render(ctx, orc, 8, 5, [(0, 0, 48, 48)], 48, 48)
+
+
+def test_render_device_packed(hip_ctx_factory):
+    torch = pytest.importorskip("torch")
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((32, 32)))
+        tiles = [(16, 0, 32, 16), (0, 16, 16, 32)]
+        rad = torch.zeros(512 * 3, device="cuda:0")
+        wt = torch.zeros(512, device="cuda:0")
+        n = ctx.render_device(4, 5, tiles, rad.data_ptr(), wt.data_ptr())
+        ctx.synchronize()
+        assert n == 512
+        orad, ow, _ = orc.render(4, 5, tiles=tiles)
+        k = 0
+        r = rad.cpu().numpy().reshape(-1, 3)
+        for (x0, y0, x1, y1) in tiles:
+            blk = orad[y0:y1, x0:x1].reshape(-1, 3)
+            assert np.array_equal(r[k:k + blk.shape[0]], blk)
+            k += blk.shape[0]
