@@ -30,15 +30,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def tiles_for_rank(W, H, tile, rank, world):
-    """Interleaved tile partition: tile k (row-major over the tile grid) -> rank k % world."""
-    out, k = [], 0
-    for y in range(0, H, tile):
-        for x in range(0, W, tile):
-            if k % world == rank:
-                out.append((x, y, min(W, x + tile), min(H, y + tile)))
-            k += 1
-    return out
+from akari_amd.dist import tiles_for_rank  # noqa: E402  (interleaved tile k -> rank k % world)
 
 
 def main():

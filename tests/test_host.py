@@ -1,0 +1,214 @@
+"""CPU-only checks of the host side: C-ABI library surface, BVH builder invariants, traversal
+builder-independence, scene language, soup generator (no GPU needed)."""
+import ctypes as C
+import re
+
+import numpy as np
+import pytest
+
+import py_oracle as O
+from akari_amd import capi, scene
+from conftest import CORNELL_MESH, ROOT
+from helpers import cornell, random_rays, small_soup
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = (ROOT / "include" / "akr_hip.h").read_text()
+    declared = set(re.findall(r"\b(akr_(?:hip|bvh)_\w+)\s*\(", hdr))
+    assert len(declared) >= 25
+    lib = C.CDLL(str(capi.LIB_PATH))
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(capi.EXPORTS) == declared, "ctypes binding out of sync with include/akr_hip.h"
+    assert capi.load_library().akr_hip_api_version() == 1
+
+
+def test_create_without_device_fails_cleanly():
+    if capi.device_count() > 0:
+        pytest.skip("a device is visible")
+    h = C.c_void_p()
+    assert capi.load_library().akr_hip_create(0, C.byref(h)) != 0 and not h.value
+    assert capi.load_library().akr_hip_last_error(None) == b"null context"
+
+
+def _check_bvh(cs, nodes, tris, max_leaf):
+    n = cs.n_tris
+    assert sorted(tris["gid"].tolist()) == list(range(n)), "every triangle in exactly one leaf"
+    v = cs.vertices[cs.indices]
+    g = tris["gid"]
+    assert np.array_equal(tris["v0"], v[g, 0])
+    assert np.array_equal(tris["e1"], (v[g, 1] - v[g, 0]).astype(np.float32))
+    assert np.array_equal(tris["e2"], (v[g, 2] - v[g, 0]).astype(np.float32))
+    # walk: child boxes contain their subtree's triangles, depth bounded, leaf sizes bounded
+    stack = [(int(nodes[0]["child"][0]), nodes[0]["bxy0"], nodes[0]["bz"][:2], 1)]
+    seen = 0
+    while stack:
+        ref, bxy, bz, depth = stack.pop()
+        assert depth <= 64
+        lo = np.array([bxy[0], bxy[2], bz[0]], np.float32)
+        hi = np.array([bxy[1], bxy[3], bz[1]], np.float32)
+        if ref & 0x80000000:
+            first, cnt = (ref & 0x7FFFFFFF) >> 3, (ref & 7) + 1
+            assert cnt <= max_leaf
+            pts = v[tris["gid"][first:first + cnt]].reshape(-1, 3)
+            assert np.all(pts >= lo) and np.all(pts <= hi)
+            seen += cnt
+        else:
+            nd = nodes[ref]
+            assert nd["axis"] < 3
+            stack.append((int(nd["child"][0]), nd["bxy0"], nd["bz"][:2], depth + 1))
+            stack.append((int(nd["child"][1]), nd["bxy1"], nd["bz"][2:], depth + 1))
+    assert seen == n
+
+
+@pytest.mark.parametrize("leaf", [1, 4, 8])
+def test_bvh_builder_invariants(leaf):
+    cs = scene.compile_scene(small_soup(20_000))
+    nodes, tris, info = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf)
+    assert info.max_leaf <= leaf and info.n_tris == cs.n_tris and info.max_depth <= 64
+    _check_bvh(cs, nodes, tris, leaf)
+
+
+def test_bvh_degenerate_inputs():
+    # identical triangles (all centroids equal) force the median split; zero-area triangles stay in
+    v = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (300, 1))
+    v[-3:] = [[0.5, 0.5, 0.5]] * 3
+    idx = np.arange(900, dtype=np.int32).reshape(-1, 3)
+    nodes, tris, info = capi.build_bvh_host(v, idx, max_leaf_size=4)
+    assert sorted(tris["gid"].tolist()) == list(range(300))
+    assert info.max_depth <= 64
+    n0, t0, _ = capi.build_bvh_host(np.zeros((0, 3), np.float32), np.zeros((0, 3), np.int32))
+    assert n0.shape[0] == 1 and t0.shape[0] == 0 and n0[0]["child"][0] == 0xFFFFFFFF
+    with pytest.raises(capi.AkrError):
+        capi.build_bvh_host(v, np.array([[0, 1, 5000]], np.int32))
+
+
+@pytest.mark.parametrize("mk", ["cornell", "soup"])
+def test_oracle_bvh_matches_brute_force(mk):
+    sc = cornell() if mk == "cornell" else small_soup(20_000)
+    cs = scene.compile_scene(sc)
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    orc = O.OracleScene(cs, nodes, tris, capi)
+    lo, hi = (-0.9, 0.9) if mk == "cornell" else (-1.1, 1.1)
+    rays = random_rays(4096, 11, lo, hi)
+    if mk == "cornell":
+        rays["o"][:, 1] += 1.0
+    bh = orc.trace_brute(rays)
+    for exact in (False, True):
+        h, nbox, ntri = orc.trace(rays, exact_cull=exact)
+        same = h["gid"] == bh["gid"]
+        assert same.mean() >= 0.9999
+        assert np.array_equal(h["t"][same], bh["t"][same])
+    _, box_exact, _ = orc.trace(rays, exact_cull=True)
+    _, box_tight, _ = orc.trace(rays, exact_cull=False)
+    assert box_tight <= box_exact
+    for any_hit in (True,):
+        ha, _, _ = orc.trace(rays, any_hit=True)
+        assert np.array_equal(ha["gid"] != 0xFFFFFFFF, bh["gid"] != 0xFFFFFFFF)
+
+
+def test_oracle_render_tight_equals_exact_cull():
+    cs = scene.compile_scene(cornell((24, 24)))
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    orc = O.OracleScene(cs, nodes, tris, capi)
+    a, wa, sa = orc.render(4, 5, exact_cull=False)
+    b, wb, sb = orc.render(4, 5, exact_cull=True)
+    assert np.array_equal(a, b) and np.array_equal(wa, wb)
+    assert sa["box_tests"] < sb["box_tests"]
+
+
+def test_oracle_render_tiles_accumulate_and_threads():
+    cs = scene.compile_scene(cornell((20, 12)))
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    orc = O.OracleScene(cs, nodes, tris, capi)
+    full, wf, _ = orc.render(3, 5, n_threads=1)
+    part = [(0, 0, 7, 12), (7, 0, 20, 5), (7, 5, 20, 12)]
+    r, w, _ = orc.render(3, 5, tiles=part, n_threads=4)
+    assert np.array_equal(full, r) and np.array_equal(wf, w)
+    r2, w2, _ = orc.render(3, 5, tiles=part, radiance=r.copy(), weight=w.copy())
+    assert np.array_equal(r2, 2 * full) and np.all(w2 == 6)
+
+
+SDL = """
+// a scene written in the reference's language (core/parser.cpp:150-363)
+let grey = [0.725, 0.71, 0.68]
+export light = EmissiveMaterial { color: [17, 12, 4] }
+export mesh = AkariMesh {
+  path: "MESH",
+  materials: [
+    DiffuseMaterial { color: [0.63, 0.065, 0.05] },
+    DiffuseMaterial { color: [0.14,0.45,0.091] },
+    DiffuseMaterial { color: $grey }, DiffuseMaterial { color: $grey }, DiffuseMaterial { color: $grey },
+    GlossyMaterial { color: 0.5, roughness: 0.3 },
+    MixMaterial { fraction: 0.25, first: DiffuseMaterial { color: $grey }, second: $light },
+    $light,
+  ]
+}
+export scene = Scene {
+    camera: PerspectiveCamera { fov: 15, position: [0, 1, 9], rotation: [0, -0.5, 0], resolution: [32, 24] },
+    integrator: Path { spp: 4, max_depth: 3, tile_size: 16, megakernel: true },
+    output: "out.png",
+    shapes: [ $mesh ]
+}
+"""
+
+
+def test_scene_language(tmp_path):
+    (tmp_path / "m.akari").write_text(SDL.replace("MESH", str(CORNELL_MESH)))
+    (tmp_path / "top.akari").write_text('import "m.akari" as cbox\nexport scene = $cbox.scene\n')
+    sc = scene.load_scene_file(tmp_path / "top.akari")
+    assert sc.camera.resolution == (32, 24) and sc.camera.fov == 15.0 and sc.camera.rotation[1] == -0.5
+    it = sc.integrator
+    assert (it.spp, it.max_depth, it.tile_size, it.wavefront) == (4, 3, 16, False)
+    mesh = sc.shapes[0]
+    assert mesh.n_tris == 36 and len(mesh.materials) == 8
+    assert mesh.materials[7] is mesh.materials[6].second      # $light is one object
+    assert not mesh.materials[7].double_sided                # the node ignores double_sided
+    assert mesh.materials[0].color.value[1] == float(np.float32(0.065))
+    cs = scene.compile_scene(sc)
+    # Emissive only at top level counts as a light (scene.cpp:62-66); the Mix child does not
+    assert [p for _, p in cs.lights] == [34, 35]
+    assert len(cs.materials) == 9
+
+
+def test_scene_language_errors(tmp_path):
+    bad = tmp_path / "bad.akari"
+    bad.write_text("export a = [1, 2\n")
+    with pytest.raises(scene.SdlError):
+        scene.load_scene_file(bad, "a")
+    bad.write_text("export a = $nothing\n")
+    with pytest.raises(scene.SdlError):
+        scene.load_scene_file(bad, "a")
+    bad.write_text('import "missing.akari" as m\n')
+    with pytest.raises(scene.SdlError):
+        scene.load_scene_file(bad, "a")
+
+
+def test_number_parsing_matches_reference():
+    p = scene.SdlParser()
+    for src, exp in (("0.725", 0 + 725 / 1000.0), ("-12.5", -12.5), ("17", 17.0), ("0.065", 65 / 1000.0)):
+        p.src, p.pos, p.path = src, 0, ROOT
+        assert p._number() == exp
+
+
+def test_soup_generator_matches_pcg():
+    v, n, t = capi.generate_soup(1000, seed=42, r=0.01, n_threads=3)
+    u = O.pcg(42, 12 * 1000).reshape(1000, 12)
+    c = (np.float32(2.0) * u[:, :3] - np.float32(1.0)).astype(np.float32)
+    off = ((np.float32(2.0) * u[:, 3:] - np.float32(1.0)) * np.float32(0.01)).astype(np.float32)
+    exp = (c[:, None, :] + off.reshape(1000, 3, 3)).astype(np.float32).reshape(-1, 3)
+    assert np.array_equal(v, exp)
+    v1, _, _ = capi.generate_soup(1000, seed=42, r=0.01, n_threads=1)
+    assert np.array_equal(v, v1)
+    assert np.array_equal(t[0], np.array([0, 1, 1, 0, 1, 1], np.float32))
+    assert np.allclose(np.linalg.norm(n.reshape(-1, 3), axis=1), 1, atol=1e-5)
+
+
+def test_soup_scene_lights():
+    cs = scene.compile_scene(scene.soup_scene(n_tris=100, resolution=(8, 8)))
+    assert cs.lights == [(0, 100), (0, 101)]
+    v = cs.vertices[cs.indices[100]]
+    ng = np.cross(v[1] - v[0], v[2] - v[0])
+    assert ng[1] < 0                      # one-sided emitter facing -y (light.h:67)
+    # power = |cross| (twice the area: 4) * texcoord area (0.5) * luminance (10), scene.cpp:72-87
+    assert np.allclose(cs.power, 4 * 0.5 * 10, rtol=1e-6)
