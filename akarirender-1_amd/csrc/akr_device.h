@@ -1,12 +1,13 @@
 // akr_device.h — device-resident scene, queue and launch-argument layouts (HBM).
 //
 // HBM layout:
-//   BVH:   akr_bvh_node[n_nodes] (64 B, DFS order) + leaf-ordered akr_bvh_tri[n] (48 B)
-//   shade: per triangle (global id order) 3 x float4 corner positions, 9 normals, 6 texcoords,
-//          material id — read once per hit, never by traversal
-//   paths: SoA per path slot: seed (u32), beta (float4), L (float4), film (float4 = rgb + weight)
-//   queues (per bounce, ping-pong): ray float4[2], slot u32; hits float4 (t, u, v, gid bits);
-//          shadow queue ray float4[2] + (colour.xyz, slot bits) float4
+//   BVH:    akr_bvh_node[n_nodes] (64 B, DFS order) + leaf-ordered akr_bvh_tri[n] (48 B)
+//   shade:  one 80-B record per triangle (global id order): v0|matid, v1|n0.x, v2|n0.y,
+//           n0.z n1, n2|pad — one gather per hit; texcoords (6 f32) only for textured scenes
+//   paths:  per slot (pixel of the tile list): seed u32, L float4, film float4 (rgb, weight)
+//   queues: per bounce (ping-pong) ray float4[2] (o|tmin, d|tmax), state float4 (beta|seed),
+//           slot u32 — path state travels with the ray, so shade reads and writes it coalesced;
+//           hits float4 (t, u, v, gid bits); shadow queue ray float4[2] + (colour|slot) float4
 #pragma once
 #include <stdint.h>
 #include <hip/hip_runtime.h>
@@ -16,9 +17,10 @@
 namespace akr {
 
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
-constexpr int kStackLds = 16;         // LDS-resident traversal stack entries per ray
+constexpr int kStackLds = 16;         // LDS-resident traversal stack entries per ray (8 B each)
 constexpr int kStackMax = 64;         // >= AKR_BVH_MAX_DEPTH
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+constexpr int kRefillMin = 16;        // refill a wave's idle lanes once at least this many are idle
 
 struct LightDev {          // AreaLight (kernel/light.h:47-57): triangle + emission texture
     float v[9];
@@ -27,13 +29,18 @@ struct LightDev {          // AreaLight (kernel/light.h:47-57): triangle + emiss
     int32_t _pad[2];
 };
 
+struct ShadeTri {          // Triangle<C> data of one global triangle id (shape.h:26-42)
+    float4 a;              // v0.xyz, material id (int bits, -1 = none)
+    float4 b;              // v1.xyz, n0.x
+    float4 c;              // v2.xyz, n0.y
+    float4 d;              // n0.z, n1.xyz
+    float4 e;              // n2.xyz, 0
+};
+
 struct SceneDev {
-    const akr_bvh_node *nodes;
-    const float4 *tris;            // akr_bvh_tri as 3 x float4
-    const float4 *corner;          // 3 per triangle: positions of the three vertices
-    const float *normals;          // 9 per triangle
-    const float *texcoords;        // 6 per triangle
-    const int32_t *matid;          // per triangle, global material or -1
+    const ShadeTri *tri;           // per global triangle id
+    const float *texcoords;        // 6 per triangle (read only when has_image_tex)
+    int32_t has_image_tex;
     const akr_material *mats;
     const akr_texture *texs;
     const float *images;
@@ -45,8 +52,6 @@ struct SceneDev {
     const float *light_func;       // n_lights
     float light_func_int;
     int32_t n_lights;
-    const uint32_t *mesh_base;     // n_meshes + 1 prefix of triangle counts
-    int32_t n_meshes;
 };
 
 struct CameraDev {
@@ -59,39 +64,43 @@ struct TraceCounters {             // reduced per wave, one atomic per wave
     unsigned long long rays, box, tri;
 };
 
-struct TraceArgs {
-    SceneDev sc;
+struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
+    const akr_bvh_node *nodes;
+    const float4 *tris;            // akr_bvh_tri as 3 x float4
     const float4 *rays;            // 2 per ray
     const uint32_t *count;         // device count (queue) or nullptr -> n
     uint32_t n;
+    uint32_t ovf_threads;          // threads covered by stack_ovf
+    uint32_t *work;                // per-launch ray counter for the dynamic fetch (zeroed before)
     float4 *hits;                  // closest: (t, u, v, gid bits)
     akr_hit *abi_hits;             // optional: write akr_hit instead
-    // shadow epilogue: colour.xyz + slot bits in .w; L accumulated per slot when unoccluded
-    const float4 *shadow_color;
-    float4 *L;
-    uint32_t *stack_ovf;           // 2 u32 per entry (ref, t bits) beyond the LDS stack
-    uint32_t ovf_threads;          // threads covered by stack_ovf
+    const uint32_t *mesh_base;     // for abi_hits: n_meshes + 1 prefix of triangle counts
+    int32_t n_meshes;
+    const float4 *shadow_color;    // shadow epilogue: colour.xyz + slot bits in .w
+    float4 *L;                     //   L[slot] += colour when unoccluded
+    uint2 *stack_ovf;              // (ref, t bits) entries beyond the LDS stack
     TraceCounters *counters;       // [3]: closest, any, shadow
 };
 
 struct ShadeArgs {
     SceneDev sc;
     const float4 *ray_in;
+    const float4 *state_in;        // beta.xyz, seed bits
     const uint32_t *slot_in;
     const float4 *hit_in;
     const uint32_t *count_in;
     float4 *ray_out;
+    float4 *state_out;
     uint32_t *slot_out;
     uint32_t *count_out;
     float4 *shadow_ray;
     float4 *shadow_color;
     uint32_t *shadow_count;
-    uint32_t *seed;
-    float4 *beta;
+    uint32_t *seed;                // per slot: written when the path ends this bounce
     float4 *L;
     int32_t depth;
     int32_t max_depth;
-    uint32_t capacity;
+    int32_t last;                  // no extension ray is traced after this bounce
 };
 
 struct RaygenArgs {
@@ -99,9 +108,9 @@ struct RaygenArgs {
     const uint32_t *pixel;         // per slot: x | y << 16
     uint32_t n;
     uint32_t *seed;
-    float4 *beta;
     float4 *L;
     float4 *ray_out;
+    float4 *state_out;
     uint32_t *slot_out;
     uint32_t *count_out;
     int32_t first_pass;

@@ -154,9 +154,10 @@ struct akr_hip_ctx {
 
     // device scene
     DBuf<akr_bvh_node> d_nodes;
-    DBuf<float4> d_tris, d_corner;
-    DBuf<float> d_normals, d_tc, d_images, d_cdf, d_func;
-    DBuf<int32_t> d_matid, d_img_w, d_img_h;
+    DBuf<float4> d_tris;
+    DBuf<ShadeTri> d_shade_tri;
+    DBuf<float> d_tc, d_images, d_cdf, d_func;
+    DBuf<int32_t> d_img_w, d_img_h;
     DBuf<int64_t> d_img_off;
     DBuf<akr_material> d_mats;
     DBuf<akr_texture> d_texs;
@@ -164,6 +165,7 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_mesh_base;
     float func_int = 0;
     int32_t n_lights = 0;
+    bool has_image_tex = false;
 
     CameraDev cam{};
     bool cam_set = false;
@@ -172,9 +174,10 @@ struct akr_hip_ctx {
     size_t cap = 0;
     std::vector<uint32_t> h_pixel;
     DBuf<uint32_t> d_pixel, d_seed, d_slot0, d_slot1, d_counts;
-    DBuf<float4> d_ray0, d_ray1, d_hit, d_sray, d_scolor, d_beta, d_L, d_film;
-    DBuf<float> d_out_rad, d_out_w;
-    DBuf<uint32_t> d_ovf;
+    DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_sray, d_scolor, d_L, d_film;
+    DBuf<uint2> d_ovf;
+    static constexpr size_t kWorkSlots = 16;
+    DBuf<uint32_t> d_work;  // dynamic-fetch counter of a standalone trace launch
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     DBuf<float4> d_trace_rays;
@@ -246,12 +249,9 @@ struct akr_hip_ctx {
 
     SceneDev scene_dev() const {
         SceneDev s{};
-        s.nodes = d_nodes.p;
-        s.tris = d_tris.p;
-        s.corner = d_corner.p;
-        s.normals = d_normals.p;
+        s.tri = d_shade_tri.p;
         s.texcoords = d_tc.p;
-        s.matid = d_matid.p;
+        s.has_image_tex = has_image_tex ? 1 : 0;
         s.mats = d_mats.p;
         s.texs = d_texs.p;
         s.images = d_images.p;
@@ -263,8 +263,6 @@ struct akr_hip_ctx {
         s.light_func = d_func.p;
         s.light_func_int = func_int;
         s.n_lights = n_lights;
-        s.mesh_base = d_mesh_base.p;
-        s.n_meshes = (int32_t)mesh_base.size() - 1;
         return s;
     }
 
@@ -287,19 +285,29 @@ struct akr_hip_ctx {
             else ok = false;
             if (!ok) throw std::runtime_error("material " + std::to_string(m) + " has an invalid type or reference");
         }
-        for (auto &t : texs)
+        has_image_tex = false;
+        for (auto &t : texs) {
             if (t.type == AKR_TEX_IMAGE && (t.image < 0 || t.image >= (int32_t)img_w.size()))
                 throw std::runtime_error("image texture references a missing image");
-        std::vector<float4> corner(3 * nt);
-        for (uint64_t g = 0; g < nt; g++)
-            for (int k = 0; k < 3; k++) {
-                const float *v = &verts[3 * (size_t)idx[3 * g + k]];
-                corner[3 * g + k] = make_float4(v[0], v[1], v[2], 0.0f);
-            }
-        d_corner.upload(corner.data(), corner.size(), stream);
-        d_normals.upload(normals.data(), normals.size(), stream);
-        d_tc.upload(texcoords.data(), texcoords.size(), stream);
-        d_matid.upload(matid.data(), matid.size(), stream);
+            has_image_tex = has_image_tex || t.type == AKR_TEX_IMAGE;
+        }
+        // one 80-byte shading record per triangle: corners, per-face-vertex normals, material
+        std::vector<ShadeTri> st(nt);
+        for (uint64_t g = 0; g < nt; g++) {
+            const float *v0 = &verts[3 * (size_t)idx[3 * g + 0]];
+            const float *v1 = &verts[3 * (size_t)idx[3 * g + 1]];
+            const float *v2 = &verts[3 * (size_t)idx[3 * g + 2]];
+            const float *nn = &normals[9 * g];
+            float mbits;
+            std::memcpy(&mbits, &matid[g], 4);
+            st[g].a = make_float4(v0[0], v0[1], v0[2], mbits);
+            st[g].b = make_float4(v1[0], v1[1], v1[2], nn[0]);
+            st[g].c = make_float4(v2[0], v2[1], v2[2], nn[1]);
+            st[g].d = make_float4(nn[2], nn[3], nn[4], nn[5]);
+            st[g].e = make_float4(nn[6], nn[7], nn[8], 0.0f);
+        }
+        d_shade_tri.upload(st.data(), st.size(), stream);
+        if (has_image_tex) d_tc.upload(texcoords.data(), texcoords.size(), stream);
         d_mats.upload(mats.data(), mats.size(), stream);
         d_texs.upload(texs.data(), texs.size(), stream);
         d_images.upload(images.data(), images.size(), stream);
@@ -353,7 +361,8 @@ struct akr_hip_ctx {
             mx = std::max(mx, trace_grid[m]);
         }
         ovf_threads = mx * kBlock;
-        d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds) * 2);
+        d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
+        d_work.reserve(kWorkSlots);
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
@@ -369,21 +378,26 @@ struct akr_hip_ctx {
         d_slot1.reserve(n);
         d_ray0.reserve(2 * n);
         d_ray1.reserve(2 * n);
+        d_state0.reserve(n);
+        d_state1.reserve(n);
         d_hit.reserve(n);
         d_sray.reserve(2 * n);
         d_scolor.reserve(n);
-        d_beta.reserve(n);
         d_L.reserve(n);
         d_film.reserve(n);
         cap = n;
     }
 
-    TraceArgs trace_args() {
+    TraceArgs trace_args(uint32_t *work) {
         TraceArgs t{};
-        t.sc = scene_dev();
+        t.nodes = d_nodes.p;
+        t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
         t.counters = d_counters.p;
+        t.work = work;
+        t.mesh_base = d_mesh_base.p;
+        t.n_meshes = (int32_t)mesh_base.size() - 1;
         return t;
     }
 
@@ -402,7 +416,8 @@ struct akr_hip_ctx {
     void trace(const float4 *rays, uint64_t n, akr_hit *hits, int any, hipStream_t st) {
         require_ready();
         if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
-        TraceArgs t = trace_args();
+        HIPCHK(hipMemsetAsync(d_work.p, 0, sizeof(uint32_t), st));
+        TraceArgs t = trace_args(d_work.p);
         t.rays = rays;
         t.n = (uint32_t)n;
         t.abi_hits = hits;
@@ -415,6 +430,7 @@ struct akr_hip_ctx {
         require_ready();
         if (!cam_set) throw std::runtime_error("camera not set (call akr_hip_set_camera)");
         if (p.spp < 0 || p.max_depth < 0) throw std::runtime_error("spp and max_depth must be >= 0");
+        if (p.max_depth > 1000) throw std::runtime_error("max_depth too large");
         if (n_tiles < 0 || (n_tiles > 0 && !tiles)) throw std::runtime_error("invalid tile list");
         h_pixel.clear();
         for (int k = 0; k < n_tiles; k++) {
@@ -426,60 +442,59 @@ struct akr_hip_ctx {
         const uint64_t N = h_pixel.size();
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
         ensure_capacity(N);
+        // counters per pass: [0, M) ray-queue counts, [M, 2M) shadow counts, [2M, 4M) work counters
         const int M = p.max_depth + 2;
-        d_counts.reserve(2 * (size_t)M);
+        d_counts.reserve(4 * (size_t)M);
         if (N == 0) return 0;
         HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
         const SceneDev sd = scene_dev();
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
-                                                             // add nothing (DESIGN.md §3): skipped
+                                                             // add nothing (DESIGN.md §3.3): skipped
         for (int s = 0; s < p.spp; s++) {
-            HIPCHK(hipMemsetAsync(d_counts.p, 0, 2 * (size_t)M * sizeof(uint32_t), st));
+            HIPCHK(hipMemsetAsync(d_counts.p, 0, 4 * (size_t)M * sizeof(uint32_t), st));
             RaygenArgs rg{};
             rg.cam = cam;
             rg.pixel = d_pixel.p;
             rg.n = (uint32_t)N;
             rg.seed = d_seed.p;
-            rg.beta = d_beta.p;
             rg.L = d_L.p;
             rg.ray_out = d_ray0.p;
+            rg.state_out = d_state0.p;
             rg.slot_out = d_slot0.p;
             rg.count_out = d_counts.p;
             rg.first_pass = s == 0;
             timed("raygen", st, [&] { launch_raygen(rg, st); });
             for (int b = 0; b < nb; b++) {
-                float4 *rin = (b & 1) ? d_ray1.p : d_ray0.p;
-                float4 *rout = (b & 1) ? d_ray0.p : d_ray1.p;
-                uint32_t *sin_ = (b & 1) ? d_slot1.p : d_slot0.p;
-                uint32_t *sout = (b & 1) ? d_slot0.p : d_slot1.p;
-                TraceArgs t = trace_args();
-                t.rays = rin;
+                const bool odd = b & 1;
+                TraceArgs t = trace_args(d_counts.p + 2 * M + 2 * b);
+                t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = d_counts.p + b;
                 t.hits = d_hit.p;
                 timed("trace_closest", st, [&] { launch_trace(TRACE_CLOSEST, count, tight, t, grid_for(TRACE_CLOSEST, N), st); });
                 ShadeArgs sh{};
                 sh.sc = sd;
-                sh.ray_in = rin;
-                sh.slot_in = sin_;
+                sh.ray_in = odd ? d_ray1.p : d_ray0.p;
+                sh.state_in = odd ? d_state1.p : d_state0.p;
+                sh.slot_in = odd ? d_slot1.p : d_slot0.p;
                 sh.hit_in = d_hit.p;
                 sh.count_in = d_counts.p + b;
-                sh.ray_out = rout;
-                sh.slot_out = sout;
+                sh.ray_out = odd ? d_ray0.p : d_ray1.p;
+                sh.state_out = odd ? d_state0.p : d_state1.p;
+                sh.slot_out = odd ? d_slot0.p : d_slot1.p;
                 sh.count_out = d_counts.p + b + 1;
                 sh.shadow_ray = d_sray.p;
                 sh.shadow_color = d_scolor.p;
                 sh.shadow_count = d_counts.p + M + b;
                 sh.seed = d_seed.p;
-                sh.beta = d_beta.p;
                 sh.L = d_L.p;
                 sh.depth = b;
                 sh.max_depth = p.max_depth;
-                sh.capacity = (uint32_t)N;
+                sh.last = b == nb - 1;
                 timed("shade", st, [&] { launch_shade(sh, (uint32_t)N, st); });
                 if (b < p.max_depth) {
-                    TraceArgs ts = trace_args();
+                    TraceArgs ts = trace_args(d_counts.p + 2 * M + 2 * b + 1);
                     ts.rays = d_sray.p;
                     ts.count = d_counts.p + M + b;
                     ts.shadow_color = d_scolor.p;

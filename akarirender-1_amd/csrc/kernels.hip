@@ -1,11 +1,12 @@
 // kernels.hip — hand-written gfx950 kernels of the wavefront path tracer.
 //
-//   k_trace<CLOSEST|ANY>  BVH2 traversal, one ray per lane, LDS-resident stack
-//                         (TBVHAccelerator::intersect / occlude, bvh-accelerator.h:488-547)
-//   k_raygen              camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86)
-//   k_shade               hit -> emission / BSDF sample / NEE light sample, wave-ballot compaction
-//                         of live paths and shadow rays (pathtracer.h:69-132)
-//   k_splat               Tile::add_sample per slot (core/film.h:66-70)
+//   k_trace<MODE,...>  BVH2 traversal, one ray per lane, LDS-resident stack, persistent waves that
+//                      refill idle lanes from the queue (TBVHAccelerator::intersect / occlude,
+//                      bvh-accelerator.h:488-547)
+//   k_raygen           camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86)
+//   k_shade            hit -> emission / BSDF sample / NEE light sample, wave-ballot compaction
+//                      of live paths and shadow rays (pathtracer.h:69-132, 137-162)
+//   k_splat            Tile::add_sample per slot (core/film.h:66-70)
 //
 // Numerics: f32 with the reference's operation order (akr_math.h); the library is built with
 // -ffp-contract=off and correctly rounded division/sqrt.
@@ -66,166 +67,195 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t lane_prefix(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Reserve `want ? 1 : 0` slots per lane of a converged wave: ballot + mbcnt prefix, one atomic.
 __device__ __forceinline__ uint32_t wave_append(bool want, uint32_t *counter) {
     unsigned long long m = __ballot(want);
-    uint32_t prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     uint32_t cnt = (uint32_t)__popcll(m);
-    unsigned long long act = __ballot(1);
-    int leader = __ffsll((long long)act) - 1;
+    int leader = __ffsll((long long)__ballot(1)) - 1;
     uint32_t base = 0;
     if ((int)__lane_id() == leader && cnt) base = atomicAdd(counter, cnt);
     base = __shfl(base, leader);
-    return base + prefix;
+    return base + lane_prefix(m);
 }
 
 // ------------------------------------------------------------------------------------- trace
-// One ray per lane.  The reference processes a node by testing its own box when it is popped;
-// here a node's two child boxes are tested when the node is visited and the far child is pushed
-// with its entry distance, which is re-compared against the current best t when popped.  Both
-// give the same visit order (near = left iff d[axis] > 0) and the same culling, hence the same
-// result as the reference traversal over the same tree.
+// One ray per lane; persistent waves.  Each loop iteration is one traversal step (an internal
+// node or a leaf) for every busy lane; a wave refills its idle lanes from the queue with one
+// atomic once at least kRefillMin of them are idle, so lanes do not wait for the slowest ray.
+//
+// Order and culling are the reference's: the reference processes a node by testing its own box
+// when it is popped; here a node's two child boxes are tested when the node is visited and the
+// far child is pushed with its entry distance, which is re-compared against the current best t
+// when popped.  Both test the same boxes against the same bounds in the same order (near = left
+// iff d[axis] > 0), hence return the same hit over the same tree.
 template <int MODE, bool COUNT, bool TIGHT>
 __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
-    __shared__ uint32_t s_ref[kStackLds * kBlock];
-    __shared__ float s_t[kStackLds * kBlock];
+    __shared__ uint2 s_stack[kStackLds * kBlock];
     const uint32_t tid = threadIdx.x;
     const uint32_t gtid = blockIdx.x * kBlock + tid;
-    const uint32_t stride = gridDim.x * kBlock;
     const uint32_t n = a.count ? *a.count : a.n;
-    const uint4 *nodes = reinterpret_cast<const uint4 *>(a.sc.nodes);
-    const float4 *nodesf = reinterpret_cast<const float4 *>(a.sc.nodes);
-    unsigned long long c_rays = 0, c_box = 0, c_tri = 0;
-
+    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
+    const uint4 *nodesu = reinterpret_cast<const uint4 *>(a.nodes);
     // virtual root (node 0): child 0 = real root with its box
     const float4 r0 = nodesf[0], r2 = nodesf[2];
-    const uint4 r3 = nodes[3];
+    const uint32_t root = nodesu[3].x;
+    unsigned long long c_rays = 0, c_box = 0, c_tri = 0;
 
-    for (uint32_t i = gtid; i < n; i += stride) {
-        const float4 ra = a.rays[2 * (size_t)i], rb = a.rays[2 * (size_t)i + 1];
-        const V3 o{ra.x, ra.y, ra.z}, d{rb.x, rb.y, rb.z};
-        const float tmin = ra.w, tmax = rb.w;
-        const V3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-        float best = kInf, bu = 0.0f, bv = 0.0f;
-        uint32_t bgid = kNoHit;
-        bool occluded = false;
-        int sp = 0;
-        uint32_t cur = r3.x;
-        if (COUNT) { c_rays++; c_box++; }
-        float troot = box_test<TIGHT>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
-        bool alive = (cur != AKR_CHILD_EMPTY) && !(troot < 0.0f || troot > (ANY ? tmax : best));
-        while (alive) {
-            if (!(cur & AKR_CHILD_LEAF)) {
-                const float4 q0 = nodesf[4 * (size_t)cur + 0];
-                const float4 q1 = nodesf[4 * (size_t)cur + 1];
-                const float4 q2 = nodesf[4 * (size_t)cur + 2];
-                const uint4 q3 = nodes[4 * (size_t)cur + 3];
-                if (COUNT) c_box += 2;
-                const float t0 = box_test<TIGHT>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
-                const float t1 = box_test<TIGHT>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
-                const float lim = ANY ? tmax : best;
-                const bool p0 = !(t0 < 0.0f || t0 > lim);
-                const bool p1 = !(t1 < 0.0f || t1 > lim);
-                const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
-                const bool left_first = dax > 0;
-                const uint32_t near_ref = left_first ? q3.x : q3.y;
-                const uint32_t far_ref = left_first ? q3.y : q3.x;
-                const bool pn = left_first ? p0 : p1;
-                const bool pf = left_first ? p1 : p0;
-                const float tf = left_first ? t1 : t0;
-                if (pn) {
-                    if (pf) {
-                        if (sp < kStackLds) {
-                            s_ref[sp * kBlock + tid] = far_ref;
-                            s_t[sp * kBlock + tid] = tf;
-                        } else {
-                            size_t e = ((size_t)(sp - kStackLds) * a.ovf_threads + gtid) * 2;
-                            a.stack_ovf[e] = far_ref;
-                            a.stack_ovf[e + 1] = fbits(tf);
-                        }
-                        sp++;
-                    }
-                    cur = near_ref;
-                    continue;
-                }
-                if (pf) {
-                    cur = far_ref;
-                    continue;
-                }
-            } else {
-                const uint32_t first = akr_leaf_first(cur), cnt = akr_leaf_count(cur);
-                for (uint32_t k = 0; k < cnt; k++) {
-                    const float4 ta = a.sc.tris[3 * (size_t)(first + k) + 0];
-                    const float4 tb = a.sc.tris[3 * (size_t)(first + k) + 1];
-                    const float4 tc = a.sc.tris[3 * (size_t)(first + k) + 2];
-                    if (COUNT) c_tri++;
-                    float t, u, v;
-                    if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
-                        best = t;
-                        bu = u;
-                        bv = v;
-                        bgid = fbits(ta.w);
-                        if (ANY) {
-                            occluded = true;
-                            break;
-                        }
+    V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
+    float tmin = 0.0f, tmax = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
+    uint32_t bgid = kNoHit, idx = 0, cur = 0;
+    int sp = 0;
+    bool busy = false, occluded = false, drained = n == 0;
+    while (true) {
+        // ---- refill idle lanes (wave-uniform control flow)
+        if (!drained) {
+            const unsigned long long idle = __ballot(!busy);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= (uint32_t)kRefillMin || nidle == (uint32_t)__popcll(__ballot(1))) {
+                const int leader = __ffsll((long long)idle) - 1;
+                uint32_t base = 0;
+                if ((int)__lane_id() == leader) base = atomicAdd(a.work, nidle);
+                base = __shfl(base, leader);
+                if (base + nidle >= n) drained = true;
+                if (!busy) {
+                    const uint32_t my = base + lane_prefix(idle);
+                    if (my < n) {
+                        idx = my;
+                        const float4 ra = a.rays[2 * (size_t)my], rb = a.rays[2 * (size_t)my + 1];
+                        o = V3{ra.x, ra.y, ra.z};
+                        d = V3{rb.x, rb.y, rb.z};
+                        tmin = ra.w;
+                        tmax = rb.w;
+                        invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                        best = kInf;
+                        bu = bv = 0.0f;
+                        bgid = kNoHit;
+                        occluded = false;
+                        sp = 0;
+                        cur = root;
+                        if (COUNT) { c_rays++; c_box++; }
+                        const float tr = box_test<TIGHT>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+                        busy = true;
+                        if (cur == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) cur = AKR_CHILD_EMPTY;
                     }
                 }
-                if (ANY && occluded) break;
             }
+        }
+        if (!__any(busy)) {
+            if (drained) break;
+            continue;
+        }
+        if (!busy) continue;
+        // ---- one traversal step
+        bool pop = false, finished = cur == AKR_CHILD_EMPTY;
+        if (finished) {
+        } else if (!(cur & AKR_CHILD_LEAF)) {
+            const float4 q0 = nodesf[4 * (size_t)cur + 0];
+            const float4 q1 = nodesf[4 * (size_t)cur + 1];
+            const float4 q2 = nodesf[4 * (size_t)cur + 2];
+            const uint4 q3 = nodesu[4 * (size_t)cur + 3];
+            if (COUNT) c_box += 2;
+            const float t0 = box_test<TIGHT>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
+            const float t1 = box_test<TIGHT>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
+            const float lim = ANY ? tmax : best;
+            const bool p0 = !(t0 < 0.0f || t0 > lim);
+            const bool p1 = !(t1 < 0.0f || t1 > lim);
+            const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
+            const bool left_first = dax > 0;
+            const uint32_t near_ref = left_first ? q3.x : q3.y;
+            const uint32_t far_ref = left_first ? q3.y : q3.x;
+            const bool pn = left_first ? p0 : p1;
+            const bool pf = left_first ? p1 : p0;
+            const float tf = left_first ? t1 : t0;
+            if (pn) {
+                if (pf) {
+                    const uint2 e = make_uint2(far_ref, fbits(tf));
+                    if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
+                    else a.stack_ovf[(size_t)(sp - kStackLds) * a.ovf_threads + gtid] = e;
+                    sp++;
+                }
+                cur = near_ref;
+            } else if (pf) {
+                cur = far_ref;
+            } else {
+                pop = true;
+            }
+        } else {
+            const uint32_t first = akr_leaf_first(cur), cnt = akr_leaf_count(cur);
+            for (uint32_t k = 0; k < cnt; k++) {
+                const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
+                const float4 tb = a.tris[3 * (size_t)(first + k) + 1];
+                const float4 tc = a.tris[3 * (size_t)(first + k) + 2];
+                if (COUNT) c_tri++;
+                float t, u, v;
+                if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
+                    best = t;
+                    bu = u;
+                    bv = v;
+                    bgid = fbits(ta.w);
+                    if (ANY) {
+                        occluded = true;
+                        break;
+                    }
+                }
+            }
+            if (ANY && occluded) finished = true;
+            else pop = true;
+        }
+        if (pop) {
             // pop, re-checking the stored entry distance against the current best
-            alive = false;
+            finished = true;
+            const float lim = ANY ? tmax : best;
             while (sp > 0) {
                 --sp;
-                uint32_t r;
-                float tt;
-                if (sp < kStackLds) {
-                    r = s_ref[sp * kBlock + tid];
-                    tt = s_t[sp * kBlock + tid];
-                } else {
-                    size_t e = ((size_t)(sp - kStackLds) * a.ovf_threads + gtid) * 2;
-                    r = a.stack_ovf[e];
-                    tt = bitsf(a.stack_ovf[e + 1]);
-                }
-                if (!(tt > (ANY ? tmax : best))) {
-                    cur = r;
-                    alive = true;
+                const uint2 e = sp < kStackLds ? s_stack[sp * kBlock + tid]
+                                               : a.stack_ovf[(size_t)(sp - kStackLds) * a.ovf_threads + gtid];
+                if (!(bitsf(e.y) > lim)) {
+                    cur = e.x;
+                    finished = false;
                     break;
                 }
             }
         }
-        if (MODE == TRACE_SHADOW) {
-            if (!occluded) {
-                const float4 c = a.shadow_color[i];
-                const uint32_t slot = fbits(c.w);
-                float4 l = a.L[slot];
-                l.x += c.x;
-                l.y += c.y;
-                l.z += c.z;
-                a.L[slot] = l;
-            }
-        } else if (a.abi_hits) {
-            akr_hit h;
-            bool hit = ANY ? occluded : (bgid != kNoHit);
-            h.t = hit ? best : kInf;
-            h.u = hit ? bu : 0.0f;
-            h.v = hit ? bv : 0.0f;
-            h.geom_id = -1;
-            h.prim_id = -1;
-            if (hit) {
-                int lo = 0, hi = a.sc.n_meshes;  // largest m with mesh_base[m] <= gid
-                while (hi - lo > 1) {
-                    int mid = (lo + hi) / 2;
-                    if (a.sc.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
+        if (finished) {
+            busy = false;
+            if (MODE == TRACE_SHADOW) {
+                if (!occluded) {
+                    const float4 c = a.shadow_color[idx];
+                    const uint32_t slot = fbits(c.w);
+                    float4 l = a.L[slot];
+                    l.x += c.x;
+                    l.y += c.y;
+                    l.z += c.z;
+                    a.L[slot] = l;
                 }
-                h.geom_id = lo;
-                h.prim_id = (int32_t)(bgid - a.sc.mesh_base[lo]);
+            } else if (a.abi_hits) {
+                akr_hit h;
+                const bool hit = ANY ? occluded : (bgid != kNoHit);
+                h.t = hit ? best : kInf;
+                h.u = hit ? bu : 0.0f;
+                h.v = hit ? bv : 0.0f;
+                h.geom_id = -1;
+                h.prim_id = -1;
+                if (hit) {
+                    int lo = 0, hi = a.n_meshes;  // largest m with mesh_base[m] <= gid
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) / 2;
+                        if (a.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
+                    }
+                    h.geom_id = lo;
+                    h.prim_id = (int32_t)(bgid - a.mesh_base[lo]);
+                }
+                h._pad[0] = h._pad[1] = h._pad[2] = 0;
+                a.abi_hits[idx] = h;
+            } else {
+                a.hits[idx] = make_float4(best, bu, bv, bitsf(bgid));
             }
-            h._pad[0] = h._pad[1] = h._pad[2] = 0;
-            a.abi_hits[i] = h;
-        } else {
-            a.hits[i] = make_float4(best, bu, bv, bitsf(bgid));
         }
     }
     if (COUNT) {
@@ -280,11 +310,10 @@ __global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
         s += a.cam.c2w[4 * k + 2] * d.z;
         rd[k] = s;
     }
-    a.seed[i] = seed;
-    a.beta[i] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     a.L[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     a.ray_out[2 * (size_t)i] = make_float4(o.x, o.y, o.z, kEps);
     a.ray_out[2 * (size_t)i + 1] = make_float4(rd[0], rd[1], rd[2], kInf);
+    a.state_out[i] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
     a.slot_out[i] = i;
     if (i == 0) *a.count_out = a.n;
 }
@@ -312,139 +341,148 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t n = *a.count_in;
     bool want_ext = false, want_sh = false;
-    float4 e0 = {}, e1 = {}, s0 = {}, s1 = {}, sc = {};
+    float4 e0 = {}, e1 = {}, st_out = {}, s0 = {}, s1 = {}, sc = {};
     uint32_t slot = 0;
     if (i < n) {
         slot = a.slot_in[i];
+        const float4 stv = a.state_in[i];
+        uint32_t seed = fbits(stv.w);
+        const V3 beta{stv.x, stv.y, stv.z};
         const float4 hv = a.hit_in[i];
         const uint32_t gid = fbits(hv.w);
-        const int32_t mid = gid != kNoHit ? a.sc.matid[gid] : -1;
-        if (mid >= 0) {  // miss -> on_miss (no-op); null material terminates (undefined in ref)
+        if (gid != kNoHit) {  // miss -> on_miss (no-op), the path ends
             const SceneDev &s = a.sc;
-            const float4 rdv = a.ray_in[2 * (size_t)i + 1];
-            const V3 wo = neg(v3(rdv.x, rdv.y, rdv.z));
-            const float u = hv.y, v = hv.z;
-            const float4 c0 = s.corner[3 * (size_t)gid + 0];
-            const float4 c1 = s.corner[3 * (size_t)gid + 1];
-            const float4 c2 = s.corner[3 * (size_t)gid + 2];
-            const V3 v0{c0.x, c0.y, c0.z}, v1{c1.x, c1.y, c1.z}, v2{c2.x, c2.y, c2.z};
-            // SurfaceInteraction(uv, triangle) (interaction.h:40-41, shape.h:31-40)
-            const V3 p = lerp3(v0, v1, v2, u, v);
-            const V3 ng = normalize(cross(sub(v1, v0), sub(v2, v0)));
-            const float *nn = s.normals + 9 * (size_t)gid;
-            const V3 ns = lerp3(ld3(nn), ld3(nn + 3), ld3(nn + 6), u, v);
-            const float *tt = s.texcoords + 6 * (size_t)gid;
-            const V2 tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
-            const akr_material *mat = &s.mats[mid];
-            uint32_t seed = a.seed[slot];
-            const float4 bv = a.beta[slot];
-            const V3 beta{bv.x, bv.y, bv.z};
-            if (mat->type == AKR_MAT_EMISSIVE) {
-                if (a.depth == 0) {
-                    const bool face_front = dot(neg(wo), ng) < 0.0f;
-                    if (mat->double_sided || face_front) {
-                        const V3 e = mul(beta, tex_eval(s, mat->color, tc));
-                        float4 l = a.L[slot];
-                        l.x += e.x;
-                        l.y += e.y;
-                        l.z += e.z;
-                        a.L[slot] = l;
+            const ShadeTri tr = s.tri[gid];
+            const int32_t mid = (int32_t)fbits(tr.a.w);
+            if (mid >= 0) {  // a null material ends the path (undefined in the reference)
+                const float4 rdv = a.ray_in[2 * (size_t)i + 1];
+                const V3 wo = neg(v3(rdv.x, rdv.y, rdv.z));
+                const float u = hv.y, v = hv.z;
+                const V3 v0{tr.a.x, tr.a.y, tr.a.z}, v1{tr.b.x, tr.b.y, tr.b.z}, v2{tr.c.x, tr.c.y, tr.c.z};
+                // SurfaceInteraction(uv, triangle) (interaction.h:40-41, shape.h:31-40)
+                const V3 p = lerp3(v0, v1, v2, u, v);
+                const V3 ng = normalize(cross(sub(v1, v0), sub(v2, v0)));
+                const V3 ns = lerp3(v3(tr.b.w, tr.c.w, tr.d.x), v3(tr.d.y, tr.d.z, tr.d.w), v3(tr.e.x, tr.e.y, tr.e.z),
+                                    u, v);
+                V2 tc{0.0f, 0.0f};  // only textures read it; constant textures ignore it
+                if (s.has_image_tex) {
+                    const float *tt = s.texcoords + 6 * (size_t)gid;
+                    tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
+                }
+                const akr_material *mat = &s.mats[mid];
+                if (mat->type == AKR_MAT_EMISSIVE) {
+                    if (a.depth == 0) {
+                        const bool face_front = dot(neg(wo), ng) < 0.0f;
+                        if (mat->double_sided || face_front) {
+                            const V3 e = mul(beta, tex_eval(s, mat->color, tc));
+                            float4 l = a.L[slot];
+                            l.x += e.x;
+                            l.y += e.y;
+                            l.z += e.z;
+                            a.L[slot] = l;
+                        }
                     }
-                }
-            } else if (a.depth < a.max_depth) {
-                // MaterialEvalContext holds a COPY of the sampler: u1.x is the next draw
-                uint32_t copy = seed;
-                float sel_u = lcg_next(copy);
-                float choice_pdf = 1.0f;
-                while (mat->type == AKR_MAT_MIX) {  // Material::select_material, material.h:251-268
-                    const float frac = tex_eval(s, mat->fraction, tc).x;
-                    if (sel_u < frac) {
-                        sel_u = sel_u / frac;
-                        mat = &s.mats[mat->second];
-                        choice_pdf *= 1.0f / frac;
-                    } else {
-                        sel_u = (sel_u - frac) / (1.0f - frac);
-                        mat = &s.mats[mat->first];
-                        choice_pdf *= 1.0f / (1.0f - frac);
+                } else if (a.depth < a.max_depth) {
+                    // MaterialEvalContext holds a COPY of the sampler: u1.x is the next draw
+                    uint32_t copy = seed;
+                    float sel_u = lcg_next(copy);
+                    float choice_pdf = 1.0f;
+                    while (mat->type == AKR_MAT_MIX) {  // Material::select_material, material.h:251-268
+                        const float frac = tex_eval(s, mat->fraction, tc).x;
+                        if (sel_u < frac) {
+                            sel_u = sel_u / frac;
+                            mat = &s.mats[mat->second];
+                            choice_pdf *= 1.0f / frac;
+                        } else {
+                            sel_u = (sel_u - frac) / (1.0f - frac);
+                            mat = &s.mats[mat->first];
+                            choice_pdf *= 1.0f / (1.0f - frac);
+                        }
                     }
-                }
-                Closure cl{CL_NONE, v3(0, 0, 0), 0.0f};
-                if (mat->type == AKR_MAT_DIFFUSE) {
-                    cl.kind = CL_DIFFUSE;
-                    cl.R = tex_eval(s, mat->color, tc);
-                } else if (mat->type == AKR_MAT_GLOSSY) {
-                    cl.kind = CL_GLOSSY;
-                    cl.R = tex_eval(s, mat->color, tc);
-                    float r = tex_eval(s, mat->roughness, tc).x;
-                    r *= r;
-                    cl.alpha = r;
-                }
-                const Frame frame = make_frame(ns);
-                const V2 bu = lcg_next2(seed);  // BSDFSampleContext(sampler.next2d(), wo)
-                if (cl.kind != CL_NONE) {
-                    V3 wi_l;
-                    float pdf = 0.0f;
-                    const V3 f = closure_sample(cl, bu, to_local(frame, wo), wi_l, pdf);
-                    const V3 wi = to_world(frame, wi_l);
-                    pdf *= choice_pdf;
-                    if (pdf != 0.0f) {
-                        const float cng = fabsf(dot(ng, wi));
-                        const V3 ev_beta = divs(muls(f, cng), pdf);
-                        // select_light(sampler.next2d()) — scene.h:79-90
-                        const V2 su = lcg_next2(seed);
-                        if (s.n_lights > 0) {
-                            int lo = 0, hi = s.n_lights + 1;  // upper_bound, distribution.h:32-44
-                            while (lo < hi) {
-                                const int m = (lo + hi) / 2;
-                                if (s.light_cdf[m] <= su.x) lo = m + 1; else hi = m;
-                            }
-                            int li = hi - 1;
-                            li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
-                            const float sel_pdf = s.light_func[li] / (s.light_func_int * (float)s.n_lights);
-                            const LightDev &lt = s.lights[li];
-                            const V2 lu = lcg_next2(seed);
-                            // AreaLight::sample (light.h:58-71)
-                            const float su0 = sqrtf(lu.x);
-                            const float b0 = 1 - su0, b1 = lu.y * su0;
-                            const V3 l0 = ld3(lt.v), l1 = ld3(lt.v + 3), l2 = ld3(lt.v + 6);
-                            const V3 lp = lerp3(l0, l1, l2, b0, b1);
-                            const V3 lx = cross(sub(l1, l0), sub(l2, l0));
-                            const V3 lng = normalize(lx);
-                            V3 lwi = sub(lp, p);
-                            const float dist_sqr = dot(lwi, lwi);
-                            lwi = divs(lwi, sqrtf(dist_sqr));
-                            const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]}, V2{lt.tc[4], lt.tc[5]}, b0, b1);
-                            const V3 Le = tex_eval(s, lt.color_tex, ltc);
-                            const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / (length(lx) * 0.5f);
-                            if (!(lpdf <= 0.0f)) {
-                                const float light_pdf = sel_pdf * lpdf;
-                                const V3 fe = closure_eval(cl, to_local(frame, wo), to_local(frame, lwi));
-                                const V3 fl = muls(mul(Le, fe), fabsf(dot(ns, lwi)));
-                                const V3 col = divs(mul(beta, fl), light_pdf);
-                                if (!is_black(col)) {
-                                    want_sh = true;
-                                    const V3 sd = neg(lwi);
-                                    s0 = make_float4(lp.x, lp.y, lp.z, kEps / fabsf(dot(lwi, lng)));
-                                    s1 = make_float4(sd.x, sd.y, sd.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
-                                    sc = make_float4(col.x, col.y, col.z, bitsf(slot));
+                    Closure cl{CL_NONE, v3(0, 0, 0), 0.0f};
+                    if (mat->type == AKR_MAT_DIFFUSE) {
+                        cl.kind = CL_DIFFUSE;
+                        cl.R = tex_eval(s, mat->color, tc);
+                    } else if (mat->type == AKR_MAT_GLOSSY) {
+                        cl.kind = CL_GLOSSY;
+                        cl.R = tex_eval(s, mat->color, tc);
+                        float r = tex_eval(s, mat->roughness, tc).x;
+                        r *= r;
+                        cl.alpha = r;
+                    }
+                    const Frame frame = make_frame(ns);
+                    const V2 bu = lcg_next2(seed);  // BSDFSampleContext(sampler.next2d(), wo)
+                    if (cl.kind != CL_NONE) {
+                        V3 wi_l;
+                        float pdf = 0.0f;
+                        const V3 f = closure_sample(cl, bu, to_local(frame, wo), wi_l, pdf);
+                        const V3 wi = to_world(frame, wi_l);
+                        pdf *= choice_pdf;
+                        if (pdf != 0.0f) {
+                            const float cng = fabsf(dot(ng, wi));
+                            const V3 ev_beta = divs(muls(f, cng), pdf);
+                            // select_light(sampler.next2d()) — scene.h:79-90
+                            const V2 su = lcg_next2(seed);
+                            if (s.n_lights > 0) {
+                                int lo = 0, hi = s.n_lights + 1;  // upper_bound, distribution.h:32-44
+                                while (lo < hi) {
+                                    const int m = (lo + hi) / 2;
+                                    if (s.light_cdf[m] <= su.x) lo = m + 1; else hi = m;
+                                }
+                                int li = hi - 1;
+                                li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
+                                const float sel_pdf = s.light_func[li] / (s.light_func_int * (float)s.n_lights);
+                                const LightDev &lt = s.lights[li];
+                                const V2 lu = lcg_next2(seed);
+                                // AreaLight::sample (light.h:58-71)
+                                const float su0 = sqrtf(lu.x);
+                                const float b0 = 1 - su0, b1 = lu.y * su0;
+                                const V3 l0 = ld3(lt.v), l1 = ld3(lt.v + 3), l2 = ld3(lt.v + 6);
+                                const V3 lp = lerp3(l0, l1, l2, b0, b1);
+                                const V3 lx = cross(sub(l1, l0), sub(l2, l0));
+                                const V3 lng = normalize(lx);
+                                V3 lwi = sub(lp, p);
+                                const float dist_sqr = dot(lwi, lwi);
+                                lwi = divs(lwi, sqrtf(dist_sqr));
+                                const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]},
+                                                     V2{lt.tc[4], lt.tc[5]}, b0, b1);
+                                const V3 Le = tex_eval(s, lt.color_tex, ltc);
+                                const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / (length(lx) * 0.5f);
+                                if (!(lpdf <= 0.0f)) {
+                                    const float light_pdf = sel_pdf * lpdf;
+                                    const V3 fe = closure_eval(cl, to_local(frame, wo), to_local(frame, lwi));
+                                    const V3 fl = muls(mul(Le, fe), fabsf(dot(ns, lwi)));
+                                    const V3 col = divs(mul(beta, fl), light_pdf);
+                                    if (!is_black(col)) {
+                                        want_sh = true;
+                                        const V3 sd = neg(lwi);
+                                        s0 = make_float4(lp.x, lp.y, lp.z, kEps / fabsf(dot(lwi, lng)));
+                                        s1 = make_float4(sd.x, sd.y, sd.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
+                                        sc = make_float4(col.x, col.y, col.z, bitsf(slot));
+                                    }
                                 }
                             }
+                            const V3 nb = mul(beta, ev_beta);
+                            if (!a.last) {
+                                want_ext = true;
+                                e0 = make_float4(p.x, p.y, p.z, kEps / cng);
+                                e1 = make_float4(wi.x, wi.y, wi.z, kInf);
+                                st_out = make_float4(nb.x, nb.y, nb.z, bitsf(seed));
+                            }
                         }
-                        const V3 nb = mul(beta, ev_beta);
-                        a.beta[slot] = make_float4(nb.x, nb.y, nb.z, 0.0f);
-                        want_ext = true;
-                        e0 = make_float4(p.x, p.y, p.z, kEps / cng);
-                        e1 = make_float4(wi.x, wi.y, wi.z, kInf);
                     }
                 }
-                a.seed[slot] = seed;
             }
         }
+        // the path does not reach another traced bounce: persist its sampler stream for the next
+        // sample pass (the stream continues across spp, cpu/integrator.cpp:124-134)
+        if (!want_ext) a.seed[slot] = seed;
     }
     const uint32_t pos = wave_append(want_ext, a.count_out);
     if (want_ext) {
         a.ray_out[2 * (size_t)pos] = e0;
         a.ray_out[2 * (size_t)pos + 1] = e1;
+        a.state_out[pos] = st_out;
         a.slot_out[pos] = slot;
     }
     const uint32_t spos = wave_append(want_sh, a.shadow_count);
