@@ -12,7 +12,7 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent.parent          # .../akarirender-1_amd
-LIB_PATH = PKG_DIR / "libakr_hip.so"
+LIB_PATH = Path(os.environ.get("AKR_HIP_LIB", PKG_DIR / "libakr_hip.so"))  # override: build variants
 GEN_PATH = PKG_DIR / "libakr_scenegen.so"
 
 

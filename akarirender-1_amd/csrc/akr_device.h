@@ -17,10 +17,16 @@
 namespace akr {
 
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
-constexpr int kStackLds = 16;         // LDS-resident traversal stack entries per ray (8 B each)
+#ifndef AKR_STACK_LDS
+#define AKR_STACK_LDS 12
+#endif
+#ifndef AKR_REFILL_MIN
+#define AKR_REFILL_MIN 32
+#endif
+constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entries per ray (8 B each)
 constexpr int kStackMax = 64;         // >= AKR_BVH_MAX_DEPTH
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
-constexpr int kRefillMin = 16;        // refill a wave's idle lanes once at least this many are idle
+constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
 
 struct LightDev {          // AreaLight (kernel/light.h:47-57): triangle + emission texture
     float v[9];

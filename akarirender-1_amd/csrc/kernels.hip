@@ -83,15 +83,32 @@ __device__ __forceinline__ uint32_t wave_append(bool want, uint32_t *counter) {
 }
 
 // ------------------------------------------------------------------------------------- trace
-// One ray per lane; persistent waves.  Each loop iteration is one traversal step (an internal
-// node or a leaf) for every busy lane; a wave refills its idle lanes from the queue with one
-// atomic once at least kRefillMin of them are idle, so lanes do not wait for the slowest ray.
-//
-// Order and culling are the reference's: the reference processes a node by testing its own box
-// when it is popped; here a node's two child boxes are tested when the node is visited and the
-// far child is pushed with its entry distance, which is re-compared against the current best t
-// when popped.  Both test the same boxes against the same bounds in the same order (near = left
-// iff d[axis] > 0), hence return the same hit over the same tree.
+__device__ __forceinline__ bool is_internal(uint32_t c) { return !(c & AKR_CHILD_LEAF); }
+__device__ __forceinline__ bool is_leaf(uint32_t c) { return (c & AKR_CHILD_LEAF) && c != AKR_CHILD_EMPTY; }
+
+// Pop the next stacked node whose stored entry distance is not beyond `lim` (the reference
+// re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
+__device__ __forceinline__ uint32_t stack_pop(const uint2 *s_stack, const uint2 *ovf, uint32_t ovf_threads,
+                                              uint32_t tid, uint32_t gtid, int &sp, float lim) {
+    while (sp > 0) {
+        --sp;
+        const uint2 e = sp < kStackLds ? s_stack[sp * kBlock + tid] : ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid];
+        if (!(__uint_as_float(e.y) > lim)) return e.x;
+    }
+    return AKR_CHILD_EMPTY;
+}
+
+// One ray per lane; persistent waves.  Per outer iteration a wave
+//   1. refills idle lanes from the queue (one atomic; the new rays' loads overlap step 2),
+//   2. runs the traversal phase: visit internal nodes until every busy lane holds a pending leaf
+//      or has run out of nodes.  A lane that finds a leaf postpones it and keeps descending
+//      (speculative traversal, Aila & Laine 2009) so it does not idle while others search,
+//   3. runs the leaf phase: Moller-Trumbore on the pending leaf of every lane.
+// Leaves are still tested in the reference's depth-first order (near = left iff d[axis] > 0);
+// speculation only visits extra internal nodes, against a stale (larger) best t, which can add
+// box tests but never a different hit.  A node's two child boxes are tested when the node is
+// visited and the far child is pushed with its entry distance, re-compared against the current
+// best when popped — the reference's pop-time test of the node's own box.
 template <int MODE, bool COUNT, bool TIGHT>
 __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
@@ -108,11 +125,14 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
 
     V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
     float tmin = 0.0f, tmax = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
-    uint32_t bgid = kNoHit, idx = 0, cur = 0;
+    uint32_t bgid = kNoHit, idx = 0, cur = AKR_CHILD_EMPTY, leaf = AKR_CHILD_EMPTY;
     int sp = 0;
     bool busy = false, occluded = false, drained = n == 0;
     while (true) {
-        // ---- refill idle lanes (wave-uniform control flow)
+        // ---- 1. refill idle lanes (wave-uniform control flow): one atomic per refill; the new
+        // rays' loads are consumed after this iteration's traversal phase, which hides them.
+        bool fresh = false;
+        float4 ra = {}, rb = {};
         if (!drained) {
             const unsigned long long idle = __ballot(!busy);
             const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -126,136 +146,126 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
                     const uint32_t my = base + lane_prefix(idle);
                     if (my < n) {
                         idx = my;
-                        const float4 ra = a.rays[2 * (size_t)my], rb = a.rays[2 * (size_t)my + 1];
-                        o = V3{ra.x, ra.y, ra.z};
-                        d = V3{rb.x, rb.y, rb.z};
-                        tmin = ra.w;
-                        tmax = rb.w;
-                        invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-                        best = kInf;
-                        bu = bv = 0.0f;
-                        bgid = kNoHit;
-                        occluded = false;
-                        sp = 0;
-                        cur = root;
-                        if (COUNT) { c_rays++; c_box++; }
-                        const float tr = box_test<TIGHT>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
-                        busy = true;
-                        if (cur == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) cur = AKR_CHILD_EMPTY;
+                        ra = a.rays[2 * (size_t)my];
+                        rb = a.rays[2 * (size_t)my + 1];
+                        fresh = true;
                     }
                 }
             }
         }
-        if (!__any(busy)) {
+        if (!__any(busy || fresh)) {
             if (drained) break;
             continue;
         }
-        if (!busy) continue;
-        // ---- one traversal step
-        bool pop = false, finished = cur == AKR_CHILD_EMPTY;
-        if (finished) {
-        } else if (!(cur & AKR_CHILD_LEAF)) {
-            const float4 q0 = nodesf[4 * (size_t)cur + 0];
-            const float4 q1 = nodesf[4 * (size_t)cur + 1];
-            const float4 q2 = nodesf[4 * (size_t)cur + 2];
-            const uint4 q3 = nodesu[4 * (size_t)cur + 3];
-            if (COUNT) c_box += 2;
-            const float t0 = box_test<TIGHT>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
-            const float t1 = box_test<TIGHT>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
-            const float lim = ANY ? tmax : best;
-            const bool p0 = !(t0 < 0.0f || t0 > lim);
-            const bool p1 = !(t1 < 0.0f || t1 > lim);
-            const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
-            const bool left_first = dax > 0;
-            const uint32_t near_ref = left_first ? q3.x : q3.y;
-            const uint32_t far_ref = left_first ? q3.y : q3.x;
-            const bool pn = left_first ? p0 : p1;
-            const bool pf = left_first ? p1 : p0;
-            const float tf = left_first ? t1 : t0;
-            if (pn) {
-                if (pf) {
-                    const uint2 e = make_uint2(far_ref, fbits(tf));
-                    if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
-                    else a.stack_ovf[(size_t)(sp - kStackLds) * a.ovf_threads + gtid] = e;
-                    sp++;
+        if (__any(busy)) {
+            // ---- 2. traversal phase
+            while (true) {
+                if (busy && is_internal(cur)) {
+                    const float4 q0 = nodesf[4 * (size_t)cur + 0];
+                    const float4 q1 = nodesf[4 * (size_t)cur + 1];
+                    const float4 q2 = nodesf[4 * (size_t)cur + 2];
+                    const uint4 q3 = nodesu[4 * (size_t)cur + 3];
+                    if (COUNT) c_box += 2;
+                    const float t0 = box_test<TIGHT>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
+                    const float t1 = box_test<TIGHT>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
+                    const float lim = ANY ? tmax : best;
+                    const bool p0 = !(t0 < 0.0f || t0 > lim);
+                    const bool p1 = !(t1 < 0.0f || t1 > lim);
+                    const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
+                    const bool left_first = dax > 0;
+                    const uint32_t near_ref = left_first ? q3.x : q3.y;
+                    const uint32_t far_ref = left_first ? q3.y : q3.x;
+                    const bool pn = left_first ? p0 : p1;
+                    const bool pf = left_first ? p1 : p0;
+                    const float tf = left_first ? t1 : t0;
+                    if (pn && pf) {
+                        const uint2 e = make_uint2(far_ref, fbits(tf));
+                        if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
+                        else a.stack_ovf[(size_t)(sp - kStackLds) * a.ovf_threads + gtid] = e;
+                        sp++;
+                    }
+                    cur = pn ? near_ref : (pf ? far_ref : stack_pop(s_stack, a.stack_ovf, a.ovf_threads, tid, gtid, sp, lim));
                 }
-                cur = near_ref;
-            } else if (pf) {
-                cur = far_ref;
-            } else {
-                pop = true;
+                if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
+                    leaf = cur;  // postpone the leaf and keep descending
+                    cur = stack_pop(s_stack, a.stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
+                }
+                if (__all(!busy || leaf != AKR_CHILD_EMPTY || cur == AKR_CHILD_EMPTY)) break;
             }
-        } else {
-            const uint32_t first = akr_leaf_first(cur), cnt = akr_leaf_count(cur);
-            for (uint32_t k = 0; k < cnt; k++) {
-                const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
-                const float4 tb = a.tris[3 * (size_t)(first + k) + 1];
-                const float4 tc = a.tris[3 * (size_t)(first + k) + 2];
-                if (COUNT) c_tri++;
-                float t, u, v;
-                if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
-                    best = t;
-                    bu = u;
-                    bv = v;
-                    bgid = fbits(ta.w);
-                    if (ANY) {
-                        occluded = true;
-                        break;
+            // ---- 3. leaf phase
+            if (busy && leaf != AKR_CHILD_EMPTY) {
+                const uint32_t first = akr_leaf_first(leaf), cnt = akr_leaf_count(leaf);
+                for (uint32_t k = 0; k < cnt; k++) {
+                    const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
+                    const float4 tb = a.tris[3 * (size_t)(first + k) + 1];
+                    const float4 tc = a.tris[3 * (size_t)(first + k) + 2];
+                    if (COUNT) c_tri++;
+                    float t, u, v;
+                    if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
+                        best = t;
+                        bu = u;
+                        bv = v;
+                        bgid = fbits(ta.w);
+                        if (ANY) {
+                            occluded = true;
+                            break;
+                        }
                     }
                 }
+                leaf = AKR_CHILD_EMPTY;
             }
-            if (ANY && occluded) finished = true;
-            else pop = true;
-        }
-        if (pop) {
-            // pop, re-checking the stored entry distance against the current best
-            finished = true;
-            const float lim = ANY ? tmax : best;
-            while (sp > 0) {
-                --sp;
-                const uint2 e = sp < kStackLds ? s_stack[sp * kBlock + tid]
-                                               : a.stack_ovf[(size_t)(sp - kStackLds) * a.ovf_threads + gtid];
-                if (!(bitsf(e.y) > lim)) {
-                    cur = e.x;
-                    finished = false;
-                    break;
-                }
-            }
-        }
-        if (finished) {
-            busy = false;
-            if (MODE == TRACE_SHADOW) {
-                if (!occluded) {
-                    const float4 c = a.shadow_color[idx];
-                    const uint32_t slot = fbits(c.w);
-                    float4 l = a.L[slot];
-                    l.x += c.x;
-                    l.y += c.y;
-                    l.z += c.z;
-                    a.L[slot] = l;
-                }
-            } else if (a.abi_hits) {
-                akr_hit h;
-                const bool hit = ANY ? occluded : (bgid != kNoHit);
-                h.t = hit ? best : kInf;
-                h.u = hit ? bu : 0.0f;
-                h.v = hit ? bv : 0.0f;
-                h.geom_id = -1;
-                h.prim_id = -1;
-                if (hit) {
-                    int lo = 0, hi = a.n_meshes;  // largest m with mesh_base[m] <= gid
-                    while (hi - lo > 1) {
-                        const int mid = (lo + hi) / 2;
-                        if (a.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
+            if (busy && ((ANY && occluded) || cur == AKR_CHILD_EMPTY)) {
+                busy = false;
+                if (MODE == TRACE_SHADOW) {
+                    if (!occluded) {
+                        const float4 c = a.shadow_color[idx];
+                        const uint32_t slot = fbits(c.w);
+                        float4 l = a.L[slot];
+                        l.x += c.x;
+                        l.y += c.y;
+                        l.z += c.z;
+                        a.L[slot] = l;
                     }
-                    h.geom_id = lo;
-                    h.prim_id = (int32_t)(bgid - a.mesh_base[lo]);
+                } else if (a.abi_hits) {
+                    akr_hit h;
+                    const bool hit = ANY ? occluded : (bgid != kNoHit);
+                    h.t = hit ? best : kInf;
+                    h.u = hit ? bu : 0.0f;
+                    h.v = hit ? bv : 0.0f;
+                    h.geom_id = -1;
+                    h.prim_id = -1;
+                    if (hit) {
+                        int lo = 0, hi = a.n_meshes;  // largest m with mesh_base[m] <= gid
+                        while (hi - lo > 1) {
+                            const int mid = (lo + hi) / 2;
+                            if (a.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
+                        }
+                        h.geom_id = lo;
+                        h.prim_id = (int32_t)(bgid - a.mesh_base[lo]);
+                    }
+                    h._pad[0] = h._pad[1] = h._pad[2] = 0;
+                    a.abi_hits[idx] = h;
+                } else {
+                    a.hits[idx] = make_float4(best, bu, bv, bitsf(bgid));
                 }
-                h._pad[0] = h._pad[1] = h._pad[2] = 0;
-                a.abi_hits[idx] = h;
-            } else {
-                a.hits[idx] = make_float4(best, bu, bv, bitsf(bgid));
             }
+        }
+        if (fresh) {
+            o = V3{ra.x, ra.y, ra.z};
+            d = V3{rb.x, rb.y, rb.z};
+            tmin = ra.w;
+            tmax = rb.w;
+            invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            best = kInf;
+            bu = bv = 0.0f;
+            bgid = kNoHit;
+            occluded = false;
+            sp = 0;
+            leaf = AKR_CHILD_EMPTY;
+            if (COUNT) { c_rays++; c_box++; }
+            const float tr = box_test<TIGHT>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+            cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
+            busy = true;
         }
     }
     if (COUNT) {

@@ -108,6 +108,25 @@ def test_trace_empty_and_device_batch(hip_ctx_factory):
         assert np.array_equal(hits_to_gid(gh, cs.mesh_base), oh["gid"])
 
 
+@pytest.mark.parametrize("n", [1, 63, 65, 1000, 100_003])
+def test_trace_each_ray_once(hip_ctx_factory, n):
+    """The persistent kernels' dynamic fetch hands every queued ray to exactly one lane."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(20_000))
+        rays = random_rays(n, 7, -1.1, 1.1)
+        ctx.set_option("count_tests", 1)
+        for any_hit in (False, True):
+            ctx.reset_stats()
+            ctx.trace(rays, any_hit=any_hit)
+            assert ctx.trace_counts()["per_mode"]["any" if any_hit else "closest"]["rays"] == n
+        # a one-bounce render traces exactly one camera ray per pixel sample
+        ctx.reset_stats()
+        ctx.render(3, 1, [(0, 0, 96, 54)], 96, 54)
+        c = ctx.trace_counts()["per_mode"]
+        assert c["closest"]["rays"] == 3 * 96 * 54
+        assert 0 < c["shadow"]["rays"] <= 3 * 96 * 54
+
+
 def _check_render(ctx, orc, spp, depth, tiles, W, H, clamp=0.0, exact=False):
     rad, w = ctx.render(spp, depth, tiles, W, H, ray_clamp=clamp, exact_cull=exact)
     orad, ow, _ = orc.render(spp, depth, tiles=tiles, ray_clamp=clamp, exact_cull=exact)
