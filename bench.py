@@ -26,8 +26,29 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic bytes per ray / AABB / triangle test
 
 
+TRACE_KERNEL_PROF_NAME = "k_trace<0, false, true>"   # closest hit, uncounted, tight cull (rocprof name)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def measured_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this same workload
+    (profiles/<tag>_traffic.json, written by tools/prof_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE rocprofv3 passes, gfx950 FETCH_SIZE x2 correction).  PMC passes cannot run inside
+    the timed region, so the figure is the profile's; (None, None) when no profile matches."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("*_traffic.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload") or {}
+        if any(w.get(k) != v for k, v in workload.items()) or kernel not in d.get("kernels", {}):
+            continue
+        best = (d["kernels"][kernel]["hbm_bytes_per_launch"], f"profiles/{p.name}")
+    return best if best else (None, None)
 
 
 from akari_amd.dist import tiles_for_rank  # noqa: E402  (interleaved tile k -> rank k % world)
@@ -46,7 +67,7 @@ def main():
     ap.add_argument("--leaf", type=int, default=4)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-frac", type=int, default=64, help="CPU sample = every n-th tile of the frame")
+    ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
     ap.add_argument("--cpu-spp", type=int, default=1)
     args = ap.parse_args()
 
@@ -134,8 +155,11 @@ def main():
     avg_ms = kc["total_ms"] / kc["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     sh = counts["per_mode"]["shadow"]
+    traffic, traffic_src = measured_traffic(TRACE_KERNEL_PROF_NAME, {
+        "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf})
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
                 "kernel": "trace_closest", "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
                 "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
                             "tri_tests": cl["tri_tests"] / max(1, cl["rays"])},

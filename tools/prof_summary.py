@@ -1,8 +1,12 @@
 """Summarise a tools/profile.sh run (rocprofv3 csv) into profiles/<tag>_summary.md + copies of the
 kernel stats / counter csvs.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and
 reads half the bytes of 128-byte-line traffic on gfx950, so traffic = 2 * FETCH_SIZE * 1024; the
-TCC_MISS_sum * 128 B column is printed beside it as the calibration check for this access pattern."""
+TCC_MISS_sum * 128 B column is printed beside it as the calibration check for this access pattern.
+WRITE_SIZE (KiB, exact for 16-B-per-lane stores and float atomics per the guide) is added unscaled.
+Also writes profiles/<tag>_traffic.json: HBM bytes per launch per kernel, which bench.py reports as
+roofline.traffic when the workload matches."""
 import csv
+import json
 import shutil
 import sys
 from collections import defaultdict
@@ -32,7 +36,7 @@ def main(tag):
                    f"{float(r['Percentage']):.2f} |")
     pmc = defaultdict(lambda: defaultdict(list))
     meta = {}
-    for sub in ("pmc_fetch", "pmc_tcc"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_tcc"):
         f = src / sub / "run_counter_collection.csv"
         if not f.exists():
             continue
@@ -44,14 +48,28 @@ def main(tag):
             meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"], r["Scratch_Size"], r["Grid_Size"])
     out += ["", "## Per-launch counters (separate `--pmc` passes, `--kernel-trace` only beside them)", "",
             "| kernel | VGPR | SGPR | LDS B | scratch | grid | FETCH_SIZE KiB | HBM read MB (2x FETCH) | "
-            "TCC_MISS x 128 B MB | L2 hit % |", "|---|---|---|---|---|---|---|---|---|---|"]
+            "WRITE_SIZE MB | TCC_MISS x 128 B MB | L2 hit % |", "|---|---|---|---|---|---|---|---|---|---|---|"]
+    traffic = {}
     for k, c in sorted(pmc.items()):
         fs = sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"]) if c["FETCH_SIZE"] else float("nan")
+        ws = sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"]) if c["WRITE_SIZE"] else 0.0
+        traffic[k] = {"hbm_bytes_per_launch": 2 * fs * 1024 + ws * 1024, "read_bytes": 2 * fs * 1024,
+                      "write_bytes": ws * 1024, "launches_sampled": len(c["FETCH_SIZE"])}
         hit = sum(c["TCC_HIT_sum"]) / max(1, len(c["TCC_HIT_sum"]))
         miss = sum(c["TCC_MISS_sum"]) / max(1, len(c["TCC_MISS_sum"]))
         m = meta[k]
         out.append(f"| {k} | {m[0]} | {m[1]} | {m[2]} | {m[3]} | {m[4]} | {fs:.0f} | {2 * fs * 1024 / 1e6:.1f} | "
-                   f"{miss * 128 / 1e6:.1f} | {100 * hit / max(1.0, hit + miss):.1f} |")
+                   f"{ws * 1024 / 1e6:.1f} | {miss * 128 / 1e6:.1f} | {100 * hit / max(1.0, hit + miss):.1f} |")
+    workload = None
+    for log in ("pmc_fetch.log",):
+        p = src / log
+        if p.exists():
+            lines = [l for l in p.read_text().splitlines() if l.startswith("{")]
+            if lines:
+                workload = json.loads(lines[-1])["config"]
+    (dst / f"{tag}_traffic.json").write_text(json.dumps(
+        {"tag": tag, "workload": workload, "source": f"profiles/{tag}_pmc_fetch.csv + {tag}_pmc_write.csv",
+         "kernels": traffic}, indent=1) + "\n")
     for log in ("kt.log",):
         p = src / log
         if p.exists():
@@ -60,7 +78,7 @@ def main(tag):
                 out += ["", "## bench.py line of the kernel-trace pass", "", "```", lines[-1], "```"]
     (dst / f"{tag}_summary.md").write_text("\n".join(out) + "\n")
     shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
-    for sub in ("pmc_fetch", "pmc_tcc"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_tcc"):
         f = src / sub / "run_counter_collection.csv"
         if f.exists():
             shutil.copy(f, dst / f"{tag}_{sub}.csv")
