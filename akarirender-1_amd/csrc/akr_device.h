@@ -27,6 +27,14 @@ constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entrie
 constexpr int kStackMax = 64;         // >= AKR_BVH_MAX_DEPTH
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
+constexpr uint32_t kWorkShards = 8;   // dynamic-fetch counters per trace launch (one per XCD group)
+constexpr uint32_t kWorkStride = 32;  // u32 between counters: each on its own 128-B line
+constexpr uint32_t kWorkWords = kWorkShards * kWorkStride;
+
+// First queue index of shard k of [0, n) (k = kWorkShards gives n).
+__host__ __device__ inline uint32_t shard_begin(uint32_t n, uint32_t k) {
+    return (uint32_t)(((uint64_t)n * k) / kWorkShards);
+}
 
 struct LightDev {          // AreaLight (kernel/light.h:47-57): triangle + emission texture
     float v[9];
@@ -77,7 +85,7 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     const uint32_t *count;         // device count (queue) or nullptr -> n
     uint32_t n;
     uint32_t ovf_threads;          // threads covered by stack_ovf
-    uint32_t *work;                // per-launch ray counter for the dynamic fetch (zeroed before)
+    uint32_t *work;                // kWorkShards dynamic-fetch counters, kWorkStride apart (zeroed before)
     float4 *hits;                  // closest: (t, u, v, gid bits)
     akr_hit *abi_hits;             // optional: write akr_hit instead
     const uint32_t *mesh_base;     // for abi_hits: n_meshes + 1 prefix of triangle counts

@@ -176,8 +176,7 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_pixel, d_seed, d_slot0, d_slot1, d_counts;
     DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_sray, d_scolor, d_L, d_film;
     DBuf<uint2> d_ovf;
-    static constexpr size_t kWorkSlots = 16;
-    DBuf<uint32_t> d_work;  // dynamic-fetch counter of a standalone trace launch
+    DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kWorkWords)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     DBuf<float4> d_trace_rays;
@@ -362,7 +361,7 @@ struct akr_hip_ctx {
         }
         ovf_threads = mx * kBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
-        d_work.reserve(kWorkSlots);
+        d_work.reserve(kWorkWords);
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
@@ -416,7 +415,7 @@ struct akr_hip_ctx {
     void trace(const float4 *rays, uint64_t n, akr_hit *hits, int any, hipStream_t st) {
         require_ready();
         if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
-        HIPCHK(hipMemsetAsync(d_work.p, 0, sizeof(uint32_t), st));
+        HIPCHK(hipMemsetAsync(d_work.p, 0, kWorkWords * sizeof(uint32_t), st));
         TraceArgs t = trace_args(d_work.p);
         t.rays = rays;
         t.n = (uint32_t)n;
@@ -442,9 +441,14 @@ struct akr_hip_ctx {
         const uint64_t N = h_pixel.size();
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
         ensure_capacity(N);
-        // counters per pass: [0, M) ray-queue counts, [M, 2M) shadow counts, [2M, 4M) work counters
+        // counters per pass, each on its own 128-B line (atomics on one line serialise):
+        // M ray-queue counts, M shadow-queue counts, then 2 trace launches x kWorkWords per bounce
         const int M = p.max_depth + 2;
-        d_counts.reserve(4 * (size_t)M);
+        const size_t n_count_words = 2 * (size_t)M * kWorkStride + 2 * (size_t)M * kWorkWords;
+        auto qcount = [&](int b) { return d_counts.p + (size_t)b * kWorkStride; };
+        auto scount = [&](int b) { return d_counts.p + (size_t)(M + b) * kWorkStride; };
+        auto work = [&](int b, int k) { return d_counts.p + 2 * (size_t)M * kWorkStride + (size_t)(2 * b + k) * kWorkWords; };
+        d_counts.reserve(n_count_words);
         if (N == 0) return 0;
         HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
@@ -453,7 +457,7 @@ struct akr_hip_ctx {
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
         for (int s = 0; s < p.spp; s++) {
-            HIPCHK(hipMemsetAsync(d_counts.p, 0, 4 * (size_t)M * sizeof(uint32_t), st));
+            HIPCHK(hipMemsetAsync(d_counts.p, 0, n_count_words * sizeof(uint32_t), st));
             RaygenArgs rg{};
             rg.cam = cam;
             rg.pixel = d_pixel.p;
@@ -463,14 +467,14 @@ struct akr_hip_ctx {
             rg.ray_out = d_ray0.p;
             rg.state_out = d_state0.p;
             rg.slot_out = d_slot0.p;
-            rg.count_out = d_counts.p;
+            rg.count_out = qcount(0);
             rg.first_pass = s == 0;
             timed("raygen", st, [&] { launch_raygen(rg, st); });
             for (int b = 0; b < nb; b++) {
                 const bool odd = b & 1;
-                TraceArgs t = trace_args(d_counts.p + 2 * M + 2 * b);
+                TraceArgs t = trace_args(work(b, 0));
                 t.rays = odd ? d_ray1.p : d_ray0.p;
-                t.count = d_counts.p + b;
+                t.count = qcount(b);
                 t.hits = d_hit.p;
                 timed("trace_closest", st, [&] { launch_trace(TRACE_CLOSEST, count, tight, t, grid_for(TRACE_CLOSEST, N), st); });
                 ShadeArgs sh{};
@@ -479,14 +483,14 @@ struct akr_hip_ctx {
                 sh.state_in = odd ? d_state1.p : d_state0.p;
                 sh.slot_in = odd ? d_slot1.p : d_slot0.p;
                 sh.hit_in = d_hit.p;
-                sh.count_in = d_counts.p + b;
+                sh.count_in = qcount(b);
                 sh.ray_out = odd ? d_ray0.p : d_ray1.p;
                 sh.state_out = odd ? d_state0.p : d_state1.p;
                 sh.slot_out = odd ? d_slot0.p : d_slot1.p;
-                sh.count_out = d_counts.p + b + 1;
+                sh.count_out = qcount(b + 1);
                 sh.shadow_ray = d_sray.p;
                 sh.shadow_color = d_scolor.p;
-                sh.shadow_count = d_counts.p + M + b;
+                sh.shadow_count = scount(b);
                 sh.seed = d_seed.p;
                 sh.L = d_L.p;
                 sh.depth = b;
@@ -494,9 +498,9 @@ struct akr_hip_ctx {
                 sh.last = b == nb - 1;
                 timed("shade", st, [&] { launch_shade(sh, (uint32_t)N, st); });
                 if (b < p.max_depth) {
-                    TraceArgs ts = trace_args(d_counts.p + 2 * M + 2 * b + 1);
+                    TraceArgs ts = trace_args(work(b, 1));
                     ts.rays = d_sray.p;
-                    ts.count = d_counts.p + M + b;
+                    ts.count = scount(b);
                     ts.shadow_color = d_scolor.p;
                     ts.L = d_L.p;
                     timed("trace_shadow", st, [&] { launch_trace(TRACE_SHADOW, count, tight, ts, grid_for(TRACE_SHADOW, N), st); });

@@ -71,15 +71,38 @@ __device__ __forceinline__ uint32_t lane_prefix(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Reserve `want ? 1 : 0` slots per lane of a converged wave: ballot + mbcnt prefix, one atomic.
-__device__ __forceinline__ uint32_t wave_append(bool want, uint32_t *counter) {
-    unsigned long long m = __ballot(want);
-    uint32_t cnt = (uint32_t)__popcll(m);
-    int leader = __ffsll((long long)__ballot(1)) - 1;
-    uint32_t base = 0;
-    if ((int)__lane_id() == leader && cnt) base = atomicAdd(counter, cnt);
-    base = __shfl(base, leader);
-    return base + lane_prefix(m);
+// Reserve `want ? 1 : 0` queue entries per thread of a whole workgroup, for two queues at once:
+// wave ballots + mbcnt prefixes, per-wave counts through LDS, one returning atomic per queue per
+// workgroup (issued by two different waves, so the two round trips overlap).  A single counter
+// word sustains only ~88 returning atomics/us chip-wide (MI355X_MICROARCH.md, dequeue), so one
+// atomic per WAVE made the shade kernel atomic-bound; per workgroup it is 4x fewer.
+// Must be reached by every thread of the block.
+__device__ __forceinline__ void block_append2(bool want_a, uint32_t *ctr_a, uint32_t &pos_a, bool want_b,
+                                              uint32_t *ctr_b, uint32_t &pos_b) {
+    constexpr int kWaves = kBlock / 64;
+    __shared__ uint32_t s_cnt[2][kWaves];
+    __shared__ uint32_t s_base[2];
+    const unsigned long long ma = __ballot(want_a), mb = __ballot(want_b);
+    const uint32_t w = threadIdx.x / 64;
+    if (__lane_id() == 0) {
+        s_cnt[0][w] = (uint32_t)__popcll(ma);
+        s_cnt[1][w] = (uint32_t)__popcll(mb);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 || threadIdx.x == 64 % kBlock) {
+        const int q = threadIdx.x == 0 ? 0 : 1;
+        uint32_t tot = 0;
+        for (int k = 0; k < kWaves; k++) tot += s_cnt[q][k];
+        s_base[q] = tot ? atomicAdd(q == 0 ? ctr_a : ctr_b, tot) : 0;
+    }
+    __syncthreads();
+    uint32_t ba = s_base[0], bb = s_base[1];
+    for (uint32_t k = 0; k < w; k++) {
+        ba += s_cnt[0][k];
+        bb += s_cnt[1][k];
+    }
+    pos_a = ba + lane_prefix(ma);
+    pos_b = bb + lane_prefix(mb);
 }
 
 // ------------------------------------------------------------------------------------- trace
@@ -128,6 +151,14 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
     uint32_t bgid = kNoHit, idx = 0, cur = AKR_CHILD_EMPTY, leaf = AKR_CHILD_EMPTY;
     int sp = 0;
     bool busy = false, occluded = false, drained = n == 0;
+    // The queue [0, n) is cut into kWorkShards contiguous ranges, each with its own counter on its
+    // own 128-B line: one counter word saturates at ~88 returning atomics/us chip-wide, so a
+    // single shared counter capped the refill rate.  A wave starts on shard blockIdx % 8 (the
+    // blocks of one XCD share it: speed only, correctness never depends on placement) and moves
+    // to the next shard when its shard is exhausted; every index is handed out exactly once.
+    uint32_t shard = blockIdx.x % kWorkShards;
+    int shards_left = kWorkShards;
+    uint32_t s_lo = shard_begin(n, shard), s_hi = shard_begin(n, shard + 1);
     while (true) {
         // ---- 1. refill idle lanes (wave-uniform control flow): one atomic per refill; the new
         // rays' loads are consumed after this iteration's traversal phase, which hides them.
@@ -139,16 +170,30 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
             if (nidle >= (uint32_t)kRefillMin || nidle == (uint32_t)__popcll(__ballot(1))) {
                 const int leader = __ffsll((long long)idle) - 1;
                 uint32_t base = 0;
-                if ((int)__lane_id() == leader) base = atomicAdd(a.work, nidle);
+                if ((int)__lane_id() == leader) base = atomicAdd(a.work + shard * kWorkStride, nidle);
                 base = __shfl(base, leader);
-                if (base + nidle >= n) drained = true;
+                const uint32_t first = s_lo + base;  // may exceed s_hi once the shard is exhausted
                 if (!busy) {
-                    const uint32_t my = base + lane_prefix(idle);
-                    if (my < n) {
+                    const uint32_t my = first + lane_prefix(idle);
+                    if (my < s_hi && base < s_hi - s_lo) {
                         idx = my;
                         ra = a.rays[2 * (size_t)my];
                         rb = a.rays[2 * (size_t)my + 1];
                         fresh = true;
+                    }
+                }
+                if (base + nidle >= s_hi - s_lo) {  // this shard is exhausted: move to the next open one
+                    while (true) {
+                        if (--shards_left == 0) {
+                            drained = true;
+                            break;
+                        }
+                        shard = (shard + 1) % kWorkShards;
+                        s_lo = shard_begin(n, shard);
+                        s_hi = shard_begin(n, shard + 1);
+                        const uint32_t taken = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                            a.work + shard * kWorkStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (taken < s_hi - s_lo) break;
                     }
                 }
             }
@@ -350,6 +395,7 @@ __device__ __forceinline__ V3 ld3(const float *p) { return v3(p[0], p[1], p[2]);
 __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t n = *a.count_in;
+    if (blockIdx.x * kBlock >= n) return;  // whole workgroup past the queue (uniform: before any barrier)
     bool want_ext = false, want_sh = false;
     float4 e0 = {}, e1 = {}, st_out = {}, s0 = {}, s1 = {}, sc = {};
     uint32_t slot = 0;
@@ -488,14 +534,14 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
         // sample pass (the stream continues across spp, cpu/integrator.cpp:124-134)
         if (!want_ext) a.seed[slot] = seed;
     }
-    const uint32_t pos = wave_append(want_ext, a.count_out);
+    uint32_t pos, spos;
+    block_append2(want_ext, a.count_out, pos, want_sh, a.shadow_count, spos);
     if (want_ext) {
         a.ray_out[2 * (size_t)pos] = e0;
         a.ray_out[2 * (size_t)pos + 1] = e1;
         a.state_out[pos] = st_out;
         a.slot_out[pos] = slot;
     }
-    const uint32_t spos = wave_append(want_sh, a.shadow_count);
     if (want_sh) {
         a.shadow_ray[2 * (size_t)spos] = s0;
         a.shadow_ray[2 * (size_t)spos + 1] = s1;
