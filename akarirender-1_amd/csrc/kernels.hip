@@ -24,18 +24,38 @@ __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); 
 // BEHIND the origin (exit m1 < tmin).  TIGHT additionally requires t <= m1 (the standard slab
 // test): it culls only boxes that cannot contain a hit with t > tmin, so it changes which nodes
 // are visited, never which triangle is the closest hit.
-template <bool TIGHT>
+template <bool TIGHT, bool FAST = false>
 __device__ __forceinline__ float box_test(float lox, float hix, float loy, float hiy, float loz, float hiz, V3 o,
                                           V3 invd, float tmin, float tmax) {
     float t0x = (lox - o.x) * invd.x, t1x = (hix - o.x) * invd.x;
     float t0y = (loy - o.y) * invd.y, t1y = (hiy - o.y) * invd.y;
     float t0z = (loz - o.z) * invd.z, t1z = (hiz - o.z) * invd.z;
-    float m0 = rmax(rmax(rmin(t0x, t1x), rmin(t0y, t1y)), rmin(t0z, t1z));
-    float m1 = rmin(rmin(rmax(t0x, t1x), rmax(t0y, t1y)), rmax(t0z, t1z));
-    float t = rmax(tmin, m0);
+    float m0, m1, t;
+    if (FAST) {
+        // Only for rays whose origin and 1/d are finite and non-zero (fast_box_ok): then no slab
+        // value is NaN, and the hardware min/max (v_min3/v_max3) select the same values as the
+        // reference's std::min/max ternaries — they can differ only in the sign of a zero, which
+        // no comparison below can see.
+        m0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        m1 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        t = fmaxf(tmin, m0);
+    } else {
+        m0 = rmax(rmax(rmin(t0x, t1x), rmin(t0y, t1y)), rmin(t0z, t1z));
+        m1 = rmin(rmin(rmax(t0x, t1x), rmax(t0y, t1y)), rmax(t0z, t1z));
+        t = rmax(tmin, m0);
+    }
     bool hit = m0 <= m1 && !(t >= tmax);
     if (TIGHT) hit = hit && t <= m1;
     return hit ? t : -1.0f;
+}
+
+// A ray whose slab values can never be NaN: finite origin, finite non-zero 1/d components, non-NaN
+// tmin/tmax
+// (0 * inf arises only from an infinite 1/d or an infinite/NaN origin; box bounds are finite or
+// the +-inf of an empty box, which a finite non-zero 1/d maps to +-inf, never NaN).
+__device__ __forceinline__ bool fast_box_ok(V3 o, V3 invd, float tmin, float tmax) {
+    return isfinite(o.x) && isfinite(o.y) && isfinite(o.z) && isfinite(invd.x) && isfinite(invd.y) &&
+           isfinite(invd.z) && invd.x != 0.0f && invd.y != 0.0f && invd.z != 0.0f && !isnan(tmin) && !isnan(tmax);
 }
 
 // MeshInstance::intersect (instance.h:42-80), Moller-Trumbore on a leaf record (v0, e1, e2).
@@ -109,16 +129,56 @@ __device__ __forceinline__ void block_append2(bool want_a, uint32_t *ctr_a, uint
 __device__ __forceinline__ bool is_internal(uint32_t c) { return !(c & AKR_CHILD_LEAF); }
 __device__ __forceinline__ bool is_leaf(uint32_t c) { return (c & AKR_CHILD_LEAF) && c != AKR_CHILD_EMPTY; }
 
+// Traversal stack pointers carry their address space in the type (LDS = 3, global = 1), so the
+// compiler cannot merge the LDS push/pop with the overflow one of the other branch into a single
+// flat (generic-address) access — which it does with plain pointers, turning every push/pop flat.
+// An entry is one u64: node ref in the low word, entry-distance bits in the high word.
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+typedef __attribute__((address_space(1))) unsigned long long glb_u64;
+
 // Pop the next stacked node whose stored entry distance is not beyond `lim` (the reference
 // re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
-__device__ __forceinline__ uint32_t stack_pop(const uint2 *s_stack, const uint2 *ovf, uint32_t ovf_threads,
+__device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_u64 *ovf, uint32_t ovf_threads,
                                               uint32_t tid, uint32_t gtid, int &sp, float lim) {
     while (sp > 0) {
         --sp;
-        const uint2 e = sp < kStackLds ? s_stack[sp * kBlock + tid] : ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid];
-        if (!(__uint_as_float(e.y) > lim)) return e.x;
+        unsigned long long e;
+        if (sp < kStackLds) e = s_stack[sp * kBlock + tid];
+        else e = ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid];
+        if (!(__uint_as_float((uint32_t)(e >> 32)) > lim)) return (uint32_t)e;
     }
     return AKR_CHILD_EMPTY;
+}
+
+// Visit internal node `cur`: test both child boxes, continue with the near one (near = left iff
+// d[axis] > 0), push the far one with its entry distance, or pop when neither is entered.
+template <bool TIGHT, bool FAST, bool ANY>
+__device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *nodesu, uint32_t &cur, V3 o, V3 d,
+                                           V3 invd, float tmin, float tmax, float best, lds_u64 *s_stack, glb_u64 *ovf,
+                                           uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
+    const float4 q0 = nodesf[4 * (size_t)cur + 0];
+    const float4 q1 = nodesf[4 * (size_t)cur + 1];
+    const float4 q2 = nodesf[4 * (size_t)cur + 2];
+    const uint4 q3 = nodesu[4 * (size_t)cur + 3];
+    const float t0 = box_test<TIGHT, FAST>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
+    const float t1 = box_test<TIGHT, FAST>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
+    const float lim = ANY ? tmax : best;
+    const bool p0 = !(t0 < 0.0f || t0 > lim);
+    const bool p1 = !(t1 < 0.0f || t1 > lim);
+    const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
+    const bool left_first = dax > 0;
+    const uint32_t near_ref = left_first ? q3.x : q3.y;
+    const uint32_t far_ref = left_first ? q3.y : q3.x;
+    const bool pn = left_first ? p0 : p1;
+    const bool pf = left_first ? p1 : p0;
+    const float tf = left_first ? t1 : t0;
+    if (pn && pf) {
+        const unsigned long long e = (unsigned long long)far_ref | ((unsigned long long)__float_as_uint(tf) << 32);
+        if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
+        else ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid] = e;
+        sp++;
+    }
+    cur = pn ? near_ref : (pf ? far_ref : stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim));
 }
 
 // One ray per lane; persistent waves.  Per outer iteration a wave
@@ -135,7 +195,9 @@ __device__ __forceinline__ uint32_t stack_pop(const uint2 *s_stack, const uint2 
 template <int MODE, bool COUNT, bool TIGHT>
 __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
-    __shared__ uint2 s_stack[kStackLds * kBlock];
+    __shared__ unsigned long long s_stack_mem[kStackLds * kBlock];
+    lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
+    glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
     const uint32_t gtid = blockIdx.x * kBlock + tid;
     const uint32_t n = a.count ? *a.count : a.n;
@@ -203,37 +265,21 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
             continue;
         }
         if (__any(busy)) {
-            // ---- 2. traversal phase
+            // ---- 2. traversal phase (fast min/max box tests unless a lane's ray could make NaNs)
+            const bool wave_fast = !__any(busy && !fast_box_ok(o, invd, tmin, tmax));
             while (true) {
                 if (busy && is_internal(cur)) {
-                    const float4 q0 = nodesf[4 * (size_t)cur + 0];
-                    const float4 q1 = nodesf[4 * (size_t)cur + 1];
-                    const float4 q2 = nodesf[4 * (size_t)cur + 2];
-                    const uint4 q3 = nodesu[4 * (size_t)cur + 3];
                     if (COUNT) c_box += 2;
-                    const float t0 = box_test<TIGHT>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
-                    const float t1 = box_test<TIGHT>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
-                    const float lim = ANY ? tmax : best;
-                    const bool p0 = !(t0 < 0.0f || t0 > lim);
-                    const bool p1 = !(t1 < 0.0f || t1 > lim);
-                    const float dax = q3.z == 0 ? d.x : (q3.z == 1 ? d.y : d.z);
-                    const bool left_first = dax > 0;
-                    const uint32_t near_ref = left_first ? q3.x : q3.y;
-                    const uint32_t far_ref = left_first ? q3.y : q3.x;
-                    const bool pn = left_first ? p0 : p1;
-                    const bool pf = left_first ? p1 : p0;
-                    const float tf = left_first ? t1 : t0;
-                    if (pn && pf) {
-                        const uint2 e = make_uint2(far_ref, fbits(tf));
-                        if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
-                        else a.stack_ovf[(size_t)(sp - kStackLds) * a.ovf_threads + gtid] = e;
-                        sp++;
-                    }
-                    cur = pn ? near_ref : (pf ? far_ref : stack_pop(s_stack, a.stack_ovf, a.ovf_threads, tid, gtid, sp, lim));
+                    if (wave_fast)
+                        visit_node<TIGHT, true, ANY>(nodesf, nodesu, cur, o, d, invd, tmin, tmax, best, s_stack,
+                                                     stack_ovf, a.ovf_threads, tid, gtid, sp);
+                    else
+                        visit_node<TIGHT, false, ANY>(nodesf, nodesu, cur, o, d, invd, tmin, tmax, best, s_stack,
+                                                      stack_ovf, a.ovf_threads, tid, gtid, sp);
                 }
                 if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
                     leaf = cur;  // postpone the leaf and keep descending
-                    cur = stack_pop(s_stack, a.stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
+                    cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
                 }
                 if (__all(!busy || leaf != AKR_CHILD_EMPTY || cur == AKR_CHILD_EMPTY)) break;
             }
