@@ -72,7 +72,8 @@ class KernelStat(C.Structure):
 
 class TraceCounts(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("box_tests", C.c_uint64), ("tri_tests", C.c_uint64),
-                ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("per_mode", (C.c_uint64 * 3) * 3)]
+                ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("per_mode", (C.c_uint64 * 3) * 3),
+                ("lane_slots", (C.c_uint64 * 3) * 3)]
 
 
 TEX_CONSTANT, TEX_IMAGE = 0, 1
@@ -325,7 +326,9 @@ class HipContext:
         c = TraceCounts()
         self._check(self.lib.akr_hip_trace_counts(self.h, C.byref(c)))
         modes = ("closest", "any", "shadow")
-        per = {m: dict(rays=c.per_mode[k][0], box_tests=c.per_mode[k][1], tri_tests=c.per_mode[k][2])
+        per = {m: dict(rays=c.per_mode[k][0], box_tests=c.per_mode[k][1], tri_tests=c.per_mode[k][2],
+                       slots_traversal=c.lane_slots[k][0], slots_busy=c.lane_slots[k][1],
+                       slots_tri=c.lane_slots[k][2])
                for k, m in enumerate(modes)}
         return dict(rays=c.rays, box_tests=c.box_tests, tri_tests=c.tri_tests, per_mode=per)
 

@@ -27,7 +27,10 @@ constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entrie
 constexpr int kStackMax = 64;         // >= AKR_BVH_MAX_DEPTH
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
-constexpr uint32_t kWorkShards = 8;   // dynamic-fetch counters per trace launch (one per XCD group)
+#ifndef AKR_WORK_SHARDS
+#define AKR_WORK_SHARDS 8
+#endif
+constexpr uint32_t kWorkShards = AKR_WORK_SHARDS;  // dynamic-fetch counters per trace launch (>= one per XCD)
 constexpr uint32_t kWorkStride = 32;  // u32 between counters: each on its own 128-B line
 constexpr uint32_t kWorkWords = kWorkShards * kWorkStride;
 
@@ -76,6 +79,7 @@ struct CameraDev {
 
 struct TraceCounters {             // reduced per wave, one atomic per wave
     unsigned long long rays, box, tri;
+    unsigned long long slots_trav, slots_leaf, slots_tri;  // lane-iterations: traversal loop, busy in it, tri loop
 };
 
 struct TraceArgs {                 // kept small: fewer SGPRs, higher residency

@@ -174,8 +174,13 @@ struct akr_hip_ctx {
     size_t cap = 0;
     std::vector<uint32_t> h_pixel;
     DBuf<uint32_t> d_pixel, d_seed, d_slot0, d_slot1, d_counts;
-    DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_sray, d_scolor, d_L, d_film;
-    DBuf<uint2> d_ovf;
+    DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_L, d_film;
+    DBuf<float4> d_sray[2], d_scolor[2];  // shadow queues, alternating by bounce
+    // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
+    // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_shade[2] = {nullptr, nullptr}, ev_shadow[2] = {nullptr, nullptr};
+    DBuf<uint2> d_ovf, d_ovf_side;  // traversal stack overflow: main-stream and side-stream traces
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kWorkWords)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
@@ -202,6 +207,10 @@ struct akr_hip_ctx {
             (void)hipEventDestroy(p.b);
         }
         for (auto e : pool) (void)hipEventDestroy(e);
+        if (side) (void)hipStreamSynchronize(side);
+        for (hipEvent_t e : {ev_fork, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1]})
+            if (e) (void)hipEventDestroy(e);
+        if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -361,7 +370,15 @@ struct akr_hip_ctx {
         }
         ovf_threads = mx * kBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
+        d_ovf_side.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_work.reserve(kWorkWords);
+    }
+
+    void ensure_side_stream() {
+        if (side) return;
+        HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        for (hipEvent_t *e : {&ev_fork, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1]})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
@@ -380,8 +397,10 @@ struct akr_hip_ctx {
         d_state0.reserve(n);
         d_state1.reserve(n);
         d_hit.reserve(n);
-        d_sray.reserve(2 * n);
-        d_scolor.reserve(n);
+        for (int k = 0; k < 2; k++) {
+            d_sray[k].reserve(2 * n);
+            d_scolor[k].reserve(n);
+        }
         d_L.reserve(n);
         d_film.reserve(n);
         cap = n;
@@ -456,8 +475,11 @@ struct akr_hip_ctx {
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
+        ensure_side_stream();
         for (int s = 0; s < p.spp; s++) {
             HIPCHK(hipMemsetAsync(d_counts.p, 0, n_count_words * sizeof(uint32_t), st));
+            HIPCHK(hipEventRecord(ev_fork, st));  // the side stream starts after this pass's memset
+            HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
             RaygenArgs rg{};
             rg.cam = cam;
             rg.pixel = d_pixel.p;
@@ -477,6 +499,8 @@ struct akr_hip_ctx {
                 t.count = qcount(b);
                 t.hits = d_hit.p;
                 timed("trace_closest", st, [&] { launch_trace(TRACE_CLOSEST, count, tight, t, grid_for(TRACE_CLOSEST, N), st); });
+                // shade(b) refills shadow queue b % 2: the shadow trace of bounce b - 2 must be done
+                if (b >= 2) HIPCHK(hipStreamWaitEvent(st, ev_shadow[odd], 0));
                 ShadeArgs sh{};
                 sh.sc = sd;
                 sh.ray_in = odd ? d_ray1.p : d_ray0.p;
@@ -488,24 +512,31 @@ struct akr_hip_ctx {
                 sh.state_out = odd ? d_state0.p : d_state1.p;
                 sh.slot_out = odd ? d_slot0.p : d_slot1.p;
                 sh.count_out = qcount(b + 1);
-                sh.shadow_ray = d_sray.p;
-                sh.shadow_color = d_scolor.p;
+                sh.shadow_ray = d_sray[odd].p;
+                sh.shadow_color = d_scolor[odd].p;
                 sh.shadow_count = scount(b);
                 sh.seed = d_seed.p;
-                sh.L = d_L.p;
+                sh.L = d_L.p;  // written at depth 0 only, before any shadow trace of the pass
                 sh.depth = b;
                 sh.max_depth = p.max_depth;
                 sh.last = b == nb - 1;
                 timed("shade", st, [&] { launch_shade(sh, (uint32_t)N, st); });
                 if (b < p.max_depth) {
+                    HIPCHK(hipEventRecord(ev_shade[odd], st));
+                    HIPCHK(hipStreamWaitEvent(side, ev_shade[odd], 0));
                     TraceArgs ts = trace_args(work(b, 1));
-                    ts.rays = d_sray.p;
+                    ts.stack_ovf = d_ovf_side.p;  // concurrent with a main-stream trace
+                    ts.rays = d_sray[odd].p;
                     ts.count = scount(b);
-                    ts.shadow_color = d_scolor.p;
+                    ts.shadow_color = d_scolor[odd].p;
                     ts.L = d_L.p;
-                    timed("trace_shadow", st, [&] { launch_trace(TRACE_SHADOW, count, tight, ts, grid_for(TRACE_SHADOW, N), st); });
+                    timed("trace_shadow", side, [&] { launch_trace(TRACE_SHADOW, count, tight, ts, grid_for(TRACE_SHADOW, N), side); });
+                    HIPCHK(hipEventRecord(ev_shadow[odd], side));
                 }
             }
+            // splat reads L, which the shadow traces accumulate into: join the side stream
+            HIPCHK(hipEventRecord(ev_fork, side));
+            HIPCHK(hipStreamWaitEvent(st, ev_fork, 0));
             SplatArgs sp{};
             sp.L = d_L.p;
             sp.film = d_film.p;
@@ -841,6 +872,9 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
             out->per_mode[m][0] = c[m].rays;
             out->per_mode[m][1] = c[m].box;
             out->per_mode[m][2] = c[m].tri;
+            out->lane_slots[m][0] = c[m].slots_trav;
+            out->lane_slots[m][1] = c[m].slots_leaf;
+            out->lane_slots[m][2] = c[m].slots_tri;
         }
     });
 }

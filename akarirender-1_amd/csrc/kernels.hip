@@ -160,6 +160,22 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
     const float4 q1 = nodesf[4 * (size_t)cur + 1];
     const float4 q2 = nodesf[4 * (size_t)cur + 2];
     const uint4 q3 = nodesu[4 * (size_t)cur + 3];
+#ifdef AKR_PROBE_EXTRA_LOAD  // bottleneck probe only: one more 16-B load per node visit
+    {
+        const float4 qx = nodesf[4 * (size_t)cur + (cur & 3)];
+        asm volatile("" ::"v"(qx.x), "v"(qx.y), "v"(qx.z), "v"(qx.w));
+    }
+#endif
+#ifdef AKR_PROBE_EXTRA_VALU  // bottleneck probe only: ~AKR_PROBE_EXTRA_VALU dependent VALU ops per visit
+    {
+        float x = q0.x;
+        for (int k = 0; k < AKR_PROBE_EXTRA_VALU; k++) {
+            x = x * 1.0001f;
+            asm volatile("" : "+v"(x));
+        }
+        asm volatile("" ::"v"(x));
+    }
+#endif
     const float t0 = box_test<TIGHT, FAST>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
     const float t1 = box_test<TIGHT, FAST>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
     const float lim = ANY ? tmax : best;
@@ -192,8 +208,13 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
 // box tests but never a different hit.  A node's two child boxes are tested when the node is
 // visited and the far child is pushed with its entry distance, re-compared against the current
 // best when popped — the reference's pop-time test of the node's own box.
+#ifdef AKR_TRACE_WAVES  // tuning variants: cap registers for this many waves per SIMD
+#define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
+#else
+#define AKR_TRACE_ATTR
+#endif
 template <int MODE, bool COUNT, bool TIGHT>
-__global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
+__global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
     __shared__ unsigned long long s_stack_mem[kStackLds * kBlock];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
@@ -206,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
     // virtual root (node 0): child 0 = real root with its box
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const uint32_t root = nodesu[3].x;
-    unsigned long long c_rays = 0, c_box = 0, c_tri = 0;
+    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0;
 
     V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
     float tmin = 0.0f, tmax = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
@@ -268,6 +289,10 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
             // ---- 2. traversal phase (fast min/max box tests unless a lane's ray could make NaNs)
             const bool wave_fast = !__any(busy && !fast_box_ok(o, invd, tmin, tmax));
             while (true) {
+                if (COUNT) {
+                    c_strav++;  // every lane of the (converged) wave
+                    c_sleaf += busy ? 1 : 0;
+                }
                 if (busy && is_internal(cur)) {
                     if (COUNT) c_box += 2;
                     if (wave_fast)
@@ -287,6 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
             if (busy && leaf != AKR_CHILD_EMPTY) {
                 const uint32_t first = akr_leaf_first(leaf), cnt = akr_leaf_count(leaf);
                 for (uint32_t k = 0; k < cnt; k++) {
+                    if (COUNT && lane_prefix(__ballot(1)) == 0) c_stri += 64;
                     const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
                     const float4 tb = a.tris[3 * (size_t)(first + k) + 1];
                     const float4 tc = a.tris[3 * (size_t)(first + k) + 2];
@@ -363,10 +389,16 @@ __global__ __launch_bounds__(kBlock) void k_trace(TraceArgs a) {
         c_rays = wave_sum(c_rays);
         c_box = wave_sum(c_box);
         c_tri = wave_sum(c_tri);
+        c_strav = wave_sum(c_strav);
+        c_sleaf = wave_sum(c_sleaf);
+        c_stri = wave_sum(c_stri);
         if (__lane_id() == 0) {
             atomicAdd(&a.counters[MODE].rays, c_rays);
             atomicAdd(&a.counters[MODE].box, c_box);
             atomicAdd(&a.counters[MODE].tri, c_tri);
+            atomicAdd(&a.counters[MODE].slots_trav, c_strav);
+            atomicAdd(&a.counters[MODE].slots_leaf, c_sleaf);
+            atomicAdd(&a.counters[MODE].slots_tri, c_stri);
         }
     }
 }

@@ -164,7 +164,13 @@ def main():
                 "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
                             "tri_tests": cl["tri_tests"] / max(1, cl["rays"])},
                 "shadow_per_ray": {"box_tests": sh["box_tests"] / max(1, sh["rays"]),
-                                   "tri_tests": sh["tri_tests"] / max(1, sh["rays"])}}
+                                   "tri_tests": sh["tri_tests"] / max(1, sh["rays"])},
+                # SIMD lane utilisation of the traversal loop (node visits per lane slot) and of
+                # the triangle loop (triangle tests per lane slot), from the counting pass
+                "lane_util": {m: {"traversal": c["box_tests"] / 2 / max(1, c["slots_traversal"]),
+                                  "holding_ray": c["slots_busy"] / max(1, c["slots_traversal"]),
+                                  "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
+                              for m, c in (("closest", cl), ("shadow", sh))}}
 
     cpu = None
     if args.cpu_baseline and world == 1:

@@ -147,6 +147,10 @@ typedef struct akr_trace_counts {
     uint64_t closest_rays;
     uint64_t shadow_rays;
     uint64_t per_mode[3][3]; /* [closest, any-hit, shadow] x [rays, box_tests, tri_tests] */
+    /* SIMD lane slots per mode: [traversal-loop lane-iterations (64 per wave-iteration), of which
+     * lanes holding a ray, triangle-loop lane-iterations]; box_tests/2 / slots[0] and
+     * tri_tests / slots[2] are lane utilisations. */
+    uint64_t lane_slots[3][3];
 } akr_trace_counts;
 
 int akr_hip_api_version(void);
