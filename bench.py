@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
     ap.add_argument("--cpu-spp", type=int, default=1)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
+                         "(prints the per-rank time; not a bench line for the driver)")
     args = ap.parse_args()
 
     import torch
@@ -94,10 +97,11 @@ def main():
     log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 
-    tiles = tiles_for_rank(W, H, args.tile, rank, world)
+    split = args.emulate_world if (args.emulate_world > 1 and world == 1) else world
+    tiles = tiles_for_rank(W, H, args.tile, rank, split)
     npix = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles)
-    maxpix = max(sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles_for_rank(W, H, args.tile, r, world))
-                 for r in range(world))
+    maxpix = max(sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles_for_rank(W, H, args.tile, r, split))
+                 for r in range(split))
     film = torch.zeros(maxpix * 4, device=dev)          # [radiance rgb (packed) | weight]
     rad, wgt = film[:maxpix * 3], film[maxpix * 3:]
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -145,6 +149,12 @@ def main():
             dist.destroy_process_group()
         return
 
+    if split != world:  # scaling probe: one rank's share of an N-way split, on this GPU
+        print(json.dumps({"probe": "emulated rank 0 of a tile split", "emulate_world": split, "rank_pixels": npix,
+                          "rank_ms_per_step": round(elapsed / K * 1e3, 3),
+                          "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3),
+                          "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3)}), flush=True)
+        return
     samples = W * H * K
     value = samples / elapsed / 1e6
     # roofline of the dominant kernel (closest-hit traversal)
