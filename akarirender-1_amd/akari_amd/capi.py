@@ -73,7 +73,7 @@ class KernelStat(C.Structure):
 class TraceCounts(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("box_tests", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("per_mode", (C.c_uint64 * 3) * 3),
-                ("lane_slots", (C.c_uint64 * 3) * 3)]
+                ("lane_slots", (C.c_uint64 * 4) * 3)]
 
 
 TEX_CONSTANT, TEX_IMAGE = 0, 1
@@ -88,8 +88,12 @@ NODE_DTYPE = np.dtype([("bxy0", np.float32, 4), ("bxy1", np.float32, 4), ("bz", 
                        ("child", np.uint32, 2), ("axis", np.uint32), ("_pad", np.uint32)])
 TRI_DTYPE = np.dtype([("v0", np.float32, 3), ("gid", np.uint32), ("e1", np.float32, 3), ("_p0", np.uint32),
                       ("e2", np.float32, 3), ("_p1", np.uint32)])
+NODE4_DTYPE = np.dtype([("origin", np.float32, 3), ("meta", np.uint32), ("child", np.uint32, 4),
+                        ("q", np.uint32, 6), ("_pad", np.uint32, 2)])
+LEAF_DTYPE = np.dtype([("lo", np.float32, 3), ("hi", np.float32, 3), ("first", np.uint32), ("count", np.uint32)])
 assert RAY_DTYPE.itemsize == 32 and HIT_DTYPE.itemsize == 32
 assert NODE_DTYPE.itemsize == 64 and TRI_DTYPE.itemsize == 48
+assert NODE4_DTYPE.itemsize == 64 and LEAF_DTYPE.itemsize == 32
 
 # Every export of include/akr_hip.h: name -> (restype, argtypes)
 _P = C.c_void_p
@@ -124,6 +128,9 @@ EXPORTS = {
     "akr_bvh_host_nodes": (_P, [_P]),
     "akr_bvh_host_tris": (_P, [_P]),
     "akr_bvh_host_free": (None, [_P]),
+    "akr_bvh_host_wide": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    "akr_bvh_host_wide_nodes": (_P, [_P]),
+    "akr_bvh_host_wide_leaves": (_P, [_P]),
 }
 
 _lib = None
@@ -151,8 +158,9 @@ def device_count() -> int:
 
 
 def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=1.0,
-                   n_threads=0):
-    """Run the product BVH builder on the host (no device): returns (nodes, tris, info)."""
+                   n_threads=0, wide=False):
+    """Run the product BVH builder on the host (no device): returns (nodes, tris, info), plus
+    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide`."""
     lib = load_library()
     v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
     i = np.ascontiguousarray(indices, np.int32).reshape(-1)
@@ -168,8 +176,20 @@ def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost
         C.memmove(nodes.ctypes.data, lib.akr_bvh_host_nodes(h), nodes.nbytes)
         if tris.nbytes:
             C.memmove(tris.ctypes.data, lib.akr_bvh_host_tris(h), tris.nbytes)
+        if wide:
+            nn, nl, root = C.c_uint64(0), C.c_uint64(0), C.c_uint32(0)
+            if lib.akr_bvh_host_wide(h, C.byref(nn), C.byref(nl), C.byref(root)) != 0:
+                raise AkrError("akr_bvh_host_wide failed")
+            wn = np.empty(nn.value, NODE4_DTYPE)
+            lv = np.empty(nl.value, LEAF_DTYPE)
+            if wn.nbytes:
+                C.memmove(wn.ctypes.data, lib.akr_bvh_host_wide_nodes(h), wn.nbytes)
+            if lv.nbytes:
+                C.memmove(lv.ctypes.data, lib.akr_bvh_host_wide_leaves(h), lv.nbytes)
     finally:
         lib.akr_bvh_host_free(h)
+    if wide:
+        return nodes, tris, info, (wn, lv, root.value)
     return nodes, tris, info
 
 
@@ -328,7 +348,7 @@ class HipContext:
         modes = ("closest", "any", "shadow")
         per = {m: dict(rays=c.per_mode[k][0], box_tests=c.per_mode[k][1], tri_tests=c.per_mode[k][2],
                        slots_traversal=c.lane_slots[k][0], slots_busy=c.lane_slots[k][1],
-                       slots_tri=c.lane_slots[k][2])
+                       slots_tri=c.lane_slots[k][2], visits=c.lane_slots[k][3])
                for k, m in enumerate(modes)}
         return dict(rays=c.rays, box_tests=c.box_tests, tri_tests=c.tri_tests, per_mode=per)
 

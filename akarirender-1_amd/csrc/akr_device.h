@@ -24,15 +24,21 @@ constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 #define AKR_REFILL_MIN 32
 #endif
 constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entries per ray (8 B each)
-constexpr int kStackMax = 64;         // >= AKR_BVH_MAX_DEPTH
+constexpr int kStackMax = 96;         // >= 3 pushes x 32 wide levels (BVH2 depth <= 64)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
+#ifndef AKR_WHILE_EXIT
+#define AKR_WHILE_EXIT 16
+#endif
+constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
 #ifndef AKR_WORK_SHARDS
 #define AKR_WORK_SHARDS 8
 #endif
 constexpr uint32_t kWorkShards = AKR_WORK_SHARDS;  // dynamic-fetch counters per trace launch (>= one per XCD)
 constexpr uint32_t kWorkStride = 32;  // u32 between counters: each on its own 128-B line
 constexpr uint32_t kWorkWords = kWorkShards * kWorkStride;
+// per trace: wide-kernel fetch counters, set-aside (slow) count, BVH2-kernel fetch counters
+constexpr uint32_t kTraceWords = 2 * kWorkWords + kWorkStride;
 
 // First queue index of shard k of [0, n) (k = kWorkShards gives n).
 __host__ __device__ inline uint32_t shard_begin(uint32_t n, uint32_t k) {
@@ -80,6 +86,7 @@ struct CameraDev {
 struct TraceCounters {             // reduced per wave, one atomic per wave
     unsigned long long rays, box, tri;
     unsigned long long slots_trav, slots_leaf, slots_tri;  // lane-iterations: traversal loop, busy in it, tri loop
+    unsigned long long visits;                             // internal-node visits
 };
 
 struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
@@ -97,6 +104,12 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     const float4 *shadow_color;    // shadow epilogue: colour.xyz + slot bits in .w
     float4 *L;                     //   L[slot] += colour when unoccluded
     uint2 *stack_ovf;              // (ref, t bits) entries beyond the LDS stack
+    const float4 *wide_nodes;      // akr_bvh4_node as 4 x float4
+    const float4 *wide_leaves;     // akr_bvh_leaf as 2 x float4
+    uint32_t wide_root;            // wide reference of the real root
+    const uint32_t *ray_index;     // optional indirection: queue entry -> ray index (BVH2 slow path)
+    uint32_t *slow_idx;            // wide kernel: rays that need the exact-NaN BVH2 path
+    uint32_t *slow_count;
     TraceCounters *counters;       // [3]: closest, any, shadow
 };
 

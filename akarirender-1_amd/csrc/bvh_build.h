@@ -30,4 +30,20 @@ struct BvhOutput {
 
 void build_bvh(const BvhInput &in, const akr_build_params &params, BvhOutput &out);
 
+// Wide view of a BVH2 (akr_bvh4_node / akr_bvh_leaf, akr_bvh_format.h).  root_ref is the wide
+// reference of the BVH2's real root (wide node 0, a leaf, or EMPTY for an empty scene).
+struct Bvh4Output {
+    std::vector<akr_bvh4_node> nodes;
+    std::vector<akr_bvh_leaf> leaves;
+    uint32_t root_ref = AKR_CHILD_EMPTY;
+    int max_depth = 0;
+};
+
+void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out);
+
+// Outward 8-bit quantization of one bound (exposed for tests): the q with fmaf(q, s, origin) on
+// the correct side of `bound`, s = 2^(e - 127).
+uint32_t quantize_lo(float bound, float origin, float s);
+uint32_t quantize_hi(float bound, float origin, float s);
+
 }  // namespace akr

@@ -151,9 +151,12 @@ struct akr_hip_ctx {
     bool accel_built = false;
     akr_accel_info info{};
     BvhOutput bvh;
+    Bvh4Output bvh4;
 
     // device scene
     DBuf<akr_bvh_node> d_nodes;
+    DBuf<akr_bvh4_node> d_wnodes;
+    DBuf<akr_bvh_leaf> d_wleaves;
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
@@ -181,7 +184,8 @@ struct akr_hip_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_shade[2] = {nullptr, nullptr}, ev_shadow[2] = {nullptr, nullptr};
     DBuf<uint2> d_ovf, d_ovf_side;  // traversal stack overflow: main-stream and side-stream traces
-    DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kWorkWords)
+    DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
+    DBuf<uint32_t> d_slow[2];  // rays the wide kernel hands to the BVH2 kernel (main, side stream)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     DBuf<float4> d_trace_rays;
@@ -190,6 +194,8 @@ struct akr_hip_ctx {
     // instrumentation
     bool stats = false, count = false;
     bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
+    int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
+    bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     DBuf<TraceCounters> d_counters;
     std::vector<hipEvent_t> pool;
     struct Pending {
@@ -371,7 +377,7 @@ struct akr_hip_ctx {
         ovf_threads = mx * kBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_ovf_side.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
-        d_work.reserve(kWorkWords);
+        d_work.reserve(kTraceWords);
     }
 
     void ensure_side_stream() {
@@ -382,7 +388,8 @@ struct akr_hip_ctx {
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
-        uint64_t need = (n + kBlock - 1) / kBlock;
+        const uint64_t per_block = (uint64_t)kBlock * (uint64_t)rays_per_lane;
+        uint64_t need = (n + per_block - 1) / per_block;
         return (uint32_t)std::min<uint64_t>(need, trace_grid[mode]);
     }
 
@@ -400,15 +407,38 @@ struct akr_hip_ctx {
         for (int k = 0; k < 2; k++) {
             d_sray[k].reserve(2 * n);
             d_scolor[k].reserve(n);
+            d_slow[k].reserve(n);
         }
         d_L.reserve(n);
         d_film.reserve(n);
         cap = n;
     }
 
+    // One trace: the wide kernel over the queue, then the BVH2 kernel over the (usually empty)
+    // list of rays the wide kernel set aside because their slab values could be NaN.  `t.work`
+    // is a kTraceWords area: wide fetch counters, the set-aside count, BVH2 fetch counters.
+    void trace_launch(int mode, bool tight, const TraceArgs &t, uint64_t n_max, uint32_t *slow, hipStream_t st) {
+        if (!wide) {
+            launch_trace(mode, count, tight, false, t, grid_for(mode, n_max), st);
+            return;
+        }
+        TraceArgs w = t;
+        w.slow_idx = slow;
+        w.slow_count = t.work + kWorkWords;
+        launch_trace(mode, count, tight, true, w, grid_for(mode, n_max), st);
+        TraceArgs s = t;
+        s.work = t.work + kWorkWords + kWorkStride;
+        s.count = w.slow_count;
+        s.ray_index = slow;
+        launch_trace(mode, count, tight, false, s, std::min<uint32_t>(grid_for(mode, n_max), 4 * (uint32_t)n_cu), st);
+    }
+
     TraceArgs trace_args(uint32_t *work) {
         TraceArgs t{};
         t.nodes = d_nodes.p;
+        t.wide_nodes = reinterpret_cast<const float4 *>(d_wnodes.p);
+        t.wide_leaves = reinterpret_cast<const float4 *>(d_wleaves.p);
+        t.wide_root = bvh4.root_ref;
         t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
@@ -434,13 +464,14 @@ struct akr_hip_ctx {
     void trace(const float4 *rays, uint64_t n, akr_hit *hits, int any, hipStream_t st) {
         require_ready();
         if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
-        HIPCHK(hipMemsetAsync(d_work.p, 0, kWorkWords * sizeof(uint32_t), st));
+        HIPCHK(hipMemsetAsync(d_work.p, 0, kTraceWords * sizeof(uint32_t), st));
+        d_slow[0].reserve(n);
         TraceArgs t = trace_args(d_work.p);
         t.rays = rays;
         t.n = (uint32_t)n;
         t.abi_hits = hits;
         int mode = any ? TRACE_ANY : TRACE_CLOSEST;
-        timed(any ? "trace_any" : "trace_closest", st, [&] { launch_trace(mode, count, !exact_cull, t, grid_for(mode, n), st); });
+        timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, d_slow[0].p, st); });
         HIPCHK(hipGetLastError());
     }
 
@@ -463,10 +494,10 @@ struct akr_hip_ctx {
         // counters per pass, each on its own 128-B line (atomics on one line serialise):
         // M ray-queue counts, M shadow-queue counts, then 2 trace launches x kWorkWords per bounce
         const int M = p.max_depth + 2;
-        const size_t n_count_words = 2 * (size_t)M * kWorkStride + 2 * (size_t)M * kWorkWords;
+        const size_t n_count_words = 2 * (size_t)M * kWorkStride + 2 * (size_t)M * kTraceWords;
         auto qcount = [&](int b) { return d_counts.p + (size_t)b * kWorkStride; };
         auto scount = [&](int b) { return d_counts.p + (size_t)(M + b) * kWorkStride; };
-        auto work = [&](int b, int k) { return d_counts.p + 2 * (size_t)M * kWorkStride + (size_t)(2 * b + k) * kWorkWords; };
+        auto work = [&](int b, int k) { return d_counts.p + 2 * (size_t)M * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
         d_counts.reserve(n_count_words);
         if (N == 0) return 0;
         HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
@@ -498,7 +529,7 @@ struct akr_hip_ctx {
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
-                timed("trace_closest", st, [&] { launch_trace(TRACE_CLOSEST, count, tight, t, grid_for(TRACE_CLOSEST, N), st); });
+                timed("trace_closest", st, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, d_slow[0].p, st); });
                 // shade(b) refills shadow queue b % 2: the shadow trace of bounce b - 2 must be done
                 if (b >= 2) HIPCHK(hipStreamWaitEvent(st, ev_shadow[odd], 0));
                 ShadeArgs sh{};
@@ -530,7 +561,7 @@ struct akr_hip_ctx {
                     ts.count = scount(b);
                     ts.shadow_color = d_scolor[odd].p;
                     ts.L = d_L.p;
-                    timed("trace_shadow", side, [&] { launch_trace(TRACE_SHADOW, count, tight, ts, grid_for(TRACE_SHADOW, N), side); });
+                    timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, d_slow[1].p, side); });
                     HIPCHK(hipEventRecord(ev_shadow[odd], side));
                 }
             }
@@ -614,6 +645,11 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->exact_cull = value != 0;
         } else if (k == "count_tests") {
             ctx->count = value != 0;
+        } else if (k == "wide") {
+            ctx->wide = value != 0;
+        } else if (k == "rays_per_lane") {
+            if (value < 1 || value > 64) throw std::runtime_error("rays_per_lane must be in [1, 64]");
+            ctx->rays_per_lane = (int)value;
         } else {
             throw std::runtime_error("unknown option '" + k + "'");
         }
@@ -703,7 +739,12 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
         build_bvh(in, p, ctx->bvh);
         auto &b = ctx->bvh;
+        build_bvh4(b.nodes, ctx->bvh4);
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
+        ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
+        ctx->d_wleaves.reserve(1);
+        ctx->d_wnodes.upload(ctx->bvh4.nodes.data(), ctx->bvh4.nodes.size(), ctx->stream);
+        ctx->d_wleaves.upload(ctx->bvh4.leaves.data(), ctx->bvh4.leaves.size(), ctx->stream);
         ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));
         ctx->info.n_nodes = b.nodes.size();
@@ -800,6 +841,8 @@ int akr_hip_render_device(akr_hip_ctx *ctx, const akr_pt_params *params, const a
 
 struct akr_bvh_host {
     BvhOutput out;
+    Bvh4Output wide;
+    bool wide_built = false;
 };
 
 int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t *indices, uint64_t n_triangles,
@@ -835,6 +878,24 @@ int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t
 const void *akr_bvh_host_nodes(const akr_bvh_host *h) { return h ? h->out.nodes.data() : nullptr; }
 const void *akr_bvh_host_tris(const akr_bvh_host *h) { return h ? h->out.tris.data() : nullptr; }
 void akr_bvh_host_free(akr_bvh_host *h) { delete h; }
+
+int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, uint32_t *root_ref) {
+    if (!h) return -1;
+    try {
+        if (!h->wide_built) {
+            build_bvh4(h->out.nodes, h->wide);
+            h->wide_built = true;
+        }
+        if (n_nodes) *n_nodes = h->wide.nodes.size();
+        if (n_leaves) *n_leaves = h->wide.leaves.size();
+        if (root_ref) *root_ref = h->wide.root_ref;
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+const void *akr_bvh_host_wide_nodes(const akr_bvh_host *h) { return h ? h->wide.nodes.data() : nullptr; }
+const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h) { return h ? h->wide.leaves.data() : nullptr; }
 
 int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n) {
     return guard(ctx, [&] {
@@ -875,6 +936,7 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
             out->lane_slots[m][0] = c[m].slots_trav;
             out->lane_slots[m][1] = c[m].slots_leaf;
             out->lane_slots[m][2] = c[m].slots_tri;
+            out->lane_slots[m][3] = c[m].visits;
         }
     });
 }

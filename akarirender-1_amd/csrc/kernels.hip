@@ -197,6 +197,84 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
     cur = pn ? near_ref : (pf ? far_ref : stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim));
 }
 
+// Visit wide node `cur` (akr_bvh4_node): test the four outward-quantized slot boxes, continue with
+// the first entered slot in the BVH2 depth-first order and push the other entered slots behind
+// it, each with its (conservative, <= exact) entry distance.  Returns the number of slot boxes
+// tested.  Only for rays with fast_box_ok(): the conservative boxes then pass whenever the exact
+// ones do (slab arithmetic is monotone in the bounds), so no leaf the BVH2 traversal reaches is
+// skipped; leaves are re-tested with their exact boxes before their triangles.
+__device__ __forceinline__ float ubyte(uint32_t w, int k) {  // v_cvt_f32_ubyte{k}
+    return (float)((w >> (8 * k)) & 0xFFu);
+}
+
+template <bool TIGHT, bool ANY>
+__device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o, V3 d, V3 invd, float tmin, float tmax,
+                                          float best, lds_u64 *s_stack, glb_u64 *ovf, uint32_t ovf_threads,
+                                          uint32_t tid, uint32_t gtid, int &sp) {
+    const uint4 *wu = reinterpret_cast<const uint4 *>(wn);
+    const float4 h = wn[4 * (size_t)cur + 0];   // origin.xyz, meta
+    const uint4 c = wu[4 * (size_t)cur + 1];    // slot refs
+    const uint4 qa = wu[4 * (size_t)cur + 2];   // qlo_x, qhi_x, qlo_y, qhi_y
+    const uint4 qb = wu[4 * (size_t)cur + 3];   // qlo_z, qhi_z
+    const uint32_t meta = __float_as_uint(h.w);
+    const float sx = __uint_as_float((meta & 0xFFu) << 23);
+    const float sy = __uint_as_float(((meta >> 8) & 0xFFu) << 23);
+    const float sz = __uint_as_float(((meta >> 16) & 0xFFu) << 23);
+    const float lim = ANY ? tmax : best;
+    float t[4];
+    bool hit[4];
+    uint32_t ref[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        // bound = fmaf(q, 2^e, origin): the product is exact, the one rounding is the builder's
+        const float lox = __builtin_fmaf(ubyte(qa.x, k), sx, h.x), hix = __builtin_fmaf(ubyte(qa.y, k), sx, h.x);
+        const float loy = __builtin_fmaf(ubyte(qa.z, k), sy, h.y), hiy = __builtin_fmaf(ubyte(qa.w, k), sy, h.y);
+        const float loz = __builtin_fmaf(ubyte(qb.x, k), sz, h.z), hiz = __builtin_fmaf(ubyte(qb.y, k), sz, h.z);
+        t[k] = box_test<TIGHT, true>(lox, hix, loy, hiy, loz, hiz, o, invd, tmin, tmax);
+        hit[k] = ref[k] != AKR_CHILD_EMPTY && !(t[k] < 0.0f || t[k] > lim);
+    }
+    const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
+                       (c.w != AKR_CHILD_EMPTY);
+    // BVH2 depth-first order: at each of the three folded nodes, near = left iff d[axis] > 0
+    const uint32_t ax = meta >> 24;
+    const float d0 = (ax & 3u) == 0 ? d.x : ((ax & 3u) == 1 ? d.y : d.z);
+    const float d1 = ((ax >> 2) & 3u) == 0 ? d.x : (((ax >> 2) & 3u) == 1 ? d.y : d.z);
+    const float d2 = ((ax >> 4) & 3u) == 0 ? d.x : (((ax >> 4) & 3u) == 1 ? d.y : d.z);
+    auto swap_slots = [&](bool sw, int i, int j) {
+        const float ti = t[i];
+        const bool hi_ = hit[i];
+        const uint32_t ri = ref[i];
+        t[i] = sw ? t[j] : ti;
+        hit[i] = sw ? hit[j] : hi_;
+        ref[i] = sw ? ref[j] : ri;
+        t[j] = sw ? ti : t[j];
+        hit[j] = sw ? hi_ : hit[j];
+        ref[j] = sw ? ri : ref[j];
+    };
+    swap_slots(!(d1 > 0), 0, 1);
+    swap_slots(!(d2 > 0), 2, 3);
+    const bool swp = !(d0 > 0);
+    swap_slots(swp, 0, 2);
+    swap_slots(swp, 1, 3);
+    uint32_t cand = AKR_CHILD_EMPTY;
+    float tc = 0.0f;
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        if (hit[k]) {
+            if (cand != AKR_CHILD_EMPTY) {
+                const unsigned long long e = (unsigned long long)cand | ((unsigned long long)__float_as_uint(tc) << 32);
+                if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
+                else ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid] = e;
+                sp++;
+            }
+            cand = ref[k];
+            tc = t[k];
+        }
+    }
+    cur = cand != AKR_CHILD_EMPTY ? cand : stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim);
+    return tested;
+}
+
 // One ray per lane; persistent waves.  Per outer iteration a wave
 //   1. refills idle lanes from the queue (one atomic; the new rays' loads overlap step 2),
 //   2. runs the traversal phase: visit internal nodes until every busy lane holds a pending leaf
@@ -213,7 +291,7 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
 #else
 #define AKR_TRACE_ATTR
 #endif
-template <int MODE, bool COUNT, bool TIGHT>
+template <int MODE, bool COUNT, bool TIGHT, bool WIDE>
 __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
     __shared__ unsigned long long s_stack_mem[kStackLds * kBlock];
@@ -226,8 +304,9 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     const uint4 *nodesu = reinterpret_cast<const uint4 *>(a.nodes);
     // virtual root (node 0): child 0 = real root with its box
     const float4 r0 = nodesf[0], r2 = nodesf[2];
-    const uint32_t root = nodesu[3].x;
-    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0;
+    const uint32_t root = WIDE ? a.wide_root : nodesu[3].x;
+    const float4 *wn = a.wide_nodes;
+    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0, c_visit = 0;
 
     V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
     float tmin = 0.0f, tmax = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
@@ -259,9 +338,9 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 if (!busy) {
                     const uint32_t my = first + lane_prefix(idle);
                     if (my < s_hi && base < s_hi - s_lo) {
-                        idx = my;
-                        ra = a.rays[2 * (size_t)my];
-                        rb = a.rays[2 * (size_t)my + 1];
+                        idx = a.ray_index ? a.ray_index[my] : my;
+                        ra = a.rays[2 * (size_t)idx];
+                        rb = a.rays[2 * (size_t)idx + 1];
                         fresh = true;
                     }
                 }
@@ -286,15 +365,26 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             continue;
         }
         if (__any(busy)) {
-            // ---- 2. traversal phase (fast min/max box tests unless a lane's ray could make NaNs)
-            const bool wave_fast = !__any(busy && !fast_box_ok(o, invd, tmin, tmax));
+            // ---- 2. traversal phase (fast min/max box tests unless a lane's ray could make NaNs;
+            // the wide kernel only ever holds rays with fast_box_ok)
+            const bool wave_fast = WIDE || !__any(busy && !fast_box_ok(o, invd, tmin, tmax));
             while (true) {
                 if (COUNT) {
                     c_strav++;  // every lane of the (converged) wave
                     c_sleaf += busy ? 1 : 0;
                 }
-                if (busy && is_internal(cur)) {
-                    if (COUNT) c_box += 2;
+                if (WIDE && busy && is_internal(cur)) {
+                    const int nt = visit_wide<TIGHT, ANY>(wn, cur, o, d, invd, tmin, tmax, best, s_stack, stack_ovf,
+                                                          a.ovf_threads, tid, gtid, sp);
+                    if (COUNT) {
+                        c_box += nt;
+                        c_visit++;
+                    }
+                } else if (!WIDE && busy && is_internal(cur)) {
+                    if (COUNT) {
+                        c_box += 2;
+                        c_visit++;
+                    }
                     if (wave_fast)
                         visit_node<TIGHT, true, ANY>(nodesf, nodesu, cur, o, d, invd, tmin, tmax, best, s_stack,
                                                      stack_ovf, a.ovf_threads, tid, gtid, sp);
@@ -306,11 +396,27 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                     leaf = cur;  // postpone the leaf and keep descending
                     cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
                 }
-                if (__all(!busy || leaf != AKR_CHILD_EMPTY || cur == AKR_CHILD_EMPTY)) break;
+                // leave for the leaf phase once at most kWhileExit lanes are still searching for
+                // their first leaf (0: every lane holds a leaf or is done — classic while-while)
+                if ((uint32_t)__popcll(__ballot(busy && leaf == AKR_CHILD_EMPTY && cur != AKR_CHILD_EMPTY)) <=
+                    (uint32_t)kWhileExit)
+                    break;
             }
             // ---- 3. leaf phase
             if (busy && leaf != AKR_CHILD_EMPTY) {
-                const uint32_t first = akr_leaf_first(leaf), cnt = akr_leaf_count(leaf);
+                uint32_t first, cnt;
+                if (WIDE) {  // the leaf's exact box, with the current best: the BVH2 pop-time test
+                    const float4 *lr = a.wide_leaves + 2 * (size_t)(leaf & 0x7FFFFFFFu);
+                    const float4 l0 = lr[0], l1 = lr[1];  // lo.xyz hi.x | hi.yz first count
+                    const float tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
+                    const bool in = !(tl < 0.0f || tl > (ANY ? tmax : best));
+                    if (COUNT) c_box++;
+                    first = fbits(l1.z);
+                    cnt = in ? fbits(l1.w) : 0u;
+                } else {
+                    first = akr_leaf_first(leaf);
+                    cnt = akr_leaf_count(leaf);
+                }
                 for (uint32_t k = 0; k < cnt; k++) {
                     if (COUNT && lane_prefix(__ballot(1)) == 0) c_stri += 64;
                     const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
@@ -373,6 +479,12 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             tmin = ra.w;
             tmax = rb.w;
             invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            if (WIDE && !fast_box_ok(o, invd, tmin, tmax)) {  // rare: the BVH2 kernel traces it
+                a.slow_idx[atomicAdd(a.slow_count, 1u)] = idx;
+                fresh = false;
+            }
+        }
+        if (fresh) {
             best = kInf;
             bu = bv = 0.0f;
             bgid = kNoHit;
@@ -380,7 +492,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             sp = 0;
             leaf = AKR_CHILD_EMPTY;
             if (COUNT) { c_rays++; c_box++; }
-            const float tr = box_test<TIGHT>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+            const float tr = box_test<TIGHT, WIDE>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
             cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
             busy = true;
         }
@@ -392,6 +504,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
         c_strav = wave_sum(c_strav);
         c_sleaf = wave_sum(c_sleaf);
         c_stri = wave_sum(c_stri);
+        c_visit = wave_sum(c_visit);
         if (__lane_id() == 0) {
             atomicAdd(&a.counters[MODE].rays, c_rays);
             atomicAdd(&a.counters[MODE].box, c_box);
@@ -399,6 +512,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             atomicAdd(&a.counters[MODE].slots_trav, c_strav);
             atomicAdd(&a.counters[MODE].slots_leaf, c_sleaf);
             atomicAdd(&a.counters[MODE].slots_tri, c_stri);
+            atomicAdd(&a.counters[MODE].visits, c_visit);
         }
     }
 }
@@ -662,33 +776,39 @@ __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint
 // ------------------------------------------------------------------------------------ launch
 static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
-template <int MODE>
+template <int MODE, bool WIDE>
 static void launch_trace_mode(bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
     if (count) {
-        if (tight) hipLaunchKernelGGL((k_trace<MODE, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_trace<MODE, true, false>), dim3(grid), dim3(kBlock), 0, st, a);
+        if (tight) hipLaunchKernelGGL((k_trace<MODE, true, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_trace<MODE, true, false, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
     } else {
-        if (tight) hipLaunchKernelGGL((k_trace<MODE, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_trace<MODE, false, false>), dim3(grid), dim3(kBlock), 0, st, a);
+        if (tight) hipLaunchKernelGGL((k_trace<MODE, false, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_trace<MODE, false, false, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
     }
 }
 
-void launch_trace(int mode, bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
+void launch_trace(int mode, bool count, bool tight, bool wide, const TraceArgs &a, uint32_t grid, hipStream_t st) {
     if (grid == 0) return;
-    if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST>(count, tight, a, grid, st);
-    else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY>(count, tight, a, grid, st);
-    else launch_trace_mode<TRACE_SHADOW>(count, tight, a, grid, st);
+    if (wide) {
+        if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, true>(count, tight, a, grid, st);
+        else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, true>(count, tight, a, grid, st);
+        else launch_trace_mode<TRACE_SHADOW, true>(count, tight, a, grid, st);
+    } else {
+        if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, false>(count, tight, a, grid, st);
+        else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, false>(count, tight, a, grid, st);
+        else launch_trace_mode<TRACE_SHADOW, false>(count, tight, a, grid, st);
+    }
 }
 
 int trace_blocks_per_cu(int mode) {
     int nb = 0;
     hipError_t e;
     if (mode == TRACE_CLOSEST)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true, true>, kBlock, 0);
     else if (mode == TRACE_ANY)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true, true>, kBlock, 0);
     else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true, true>, kBlock, 0);
     if (e != hipSuccess || nb <= 0) nb = 1;
     return nb;
 }

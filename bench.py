@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
     ap.add_argument("--cpu-spp", type=int, default=1)
+    ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
+    ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -94,6 +96,9 @@ def main():
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
     info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, n_threads=min(16, os.cpu_count() or 1))
+    if args.rays_per_lane != 1:
+        ctx.set_option("rays_per_lane", args.rays_per_lane)
+    ctx.set_option("wide", args.wide)
     log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 
@@ -172,12 +177,13 @@ def main():
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
                 "kernel": "trace_closest", "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
                 "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
+                            "node_visits": cl["visits"] / max(1, cl["rays"]),
                             "tri_tests": cl["tri_tests"] / max(1, cl["rays"])},
                 "shadow_per_ray": {"box_tests": sh["box_tests"] / max(1, sh["rays"]),
                                    "tri_tests": sh["tri_tests"] / max(1, sh["rays"])},
                 # SIMD lane utilisation of the traversal loop (node visits per lane slot) and of
                 # the triangle loop (triangle tests per lane slot), from the counting pass
-                "lane_util": {m: {"traversal": c["box_tests"] / 2 / max(1, c["slots_traversal"]),
+                "lane_util": {m: {"traversal": c["visits"] / max(1, c["slots_traversal"]),
                                   "holding_ray": c["slots_busy"] / max(1, c["slots_traversal"]),
                                   "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
                               for m, c in (("closest", cl), ("shadow", sh))}}

@@ -47,6 +47,30 @@ typedef struct akr_bvh_tri {
     uint32_t _pad1;
 } akr_bvh_tri;
 
+/* Wide (4-child) view of the same tree, which the traversal kernels walk.
+ * A wide node is one BVH2 node with its two children collapsed into it: slots 0, 1 are the left
+ * child's children (or the left child itself, slot 1 EMPTY, when it is a leaf), slots 2, 3 the
+ * right child's; axis0/1/2 are the split axes of the three BVH2 nodes, so the BVH2 depth-first
+ * order of the four slots follows from the ray direction.  Slot boxes are quantized OUTWARD to
+ * 8 bits per bound: bound = fmaf(q, 2^(e - 127), origin) is <= (lo) / >= (hi) the exact bound, so
+ * a slot test can only pass more often than the exact one.  Every leaf keeps its exact f32 box in
+ * an akr_bvh_leaf record and is tested with it (with the current best t) before its triangles:
+ * the leaves whose triangles are tested, and their order, are exactly the BVH2 traversal's. */
+typedef struct akr_bvh4_node {
+    float origin[3];
+    uint32_t meta;     /* ex | ey << 8 | ez << 16 | (axis0 | axis1 << 2 | axis2 << 4) << 24 */
+    uint32_t child[4]; /* wide node index, AKR_CHILD_LEAF | leaf index, or AKR_CHILD_EMPTY */
+    uint32_t q[6];     /* qlo_x, qhi_x, qlo_y, qhi_y, qlo_z, qhi_z; byte k of each = slot k */
+    uint32_t _pad[2];
+} akr_bvh4_node;
+
+typedef struct akr_bvh_leaf {
+    float lo[3];
+    float hi[3];
+    uint32_t first; /* into the leaf-ordered akr_bvh_tri array */
+    uint32_t count;
+} akr_bvh_leaf;
+
 static inline AKR_HD int akr_child_is_leaf(uint32_t c) { return c != AKR_CHILD_EMPTY && (c & AKR_CHILD_LEAF); }
 static inline AKR_HD uint32_t akr_leaf_first(uint32_t c) { return (c & 0x7FFFFFFFu) >> 3; }
 static inline AKR_HD uint32_t akr_leaf_count(uint32_t c) { return (c & 7u) + 1u; }

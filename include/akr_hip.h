@@ -148,9 +148,9 @@ typedef struct akr_trace_counts {
     uint64_t shadow_rays;
     uint64_t per_mode[3][3]; /* [closest, any-hit, shadow] x [rays, box_tests, tri_tests] */
     /* SIMD lane slots per mode: [traversal-loop lane-iterations (64 per wave-iteration), of which
-     * lanes holding a ray, triangle-loop lane-iterations]; box_tests/2 / slots[0] and
+     * lanes holding a ray, triangle-loop lane-iterations, node visits]; visits / slots[0] and
      * tri_tests / slots[2] are lane utilisations. */
-    uint64_t lane_slots[3][3];
+    uint64_t lane_slots[3][4];
 } akr_trace_counts;
 
 int akr_hip_api_version(void);
@@ -206,6 +206,11 @@ int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t
 const void *akr_bvh_host_nodes(const akr_bvh_host *h);
 const void *akr_bvh_host_tris(const akr_bvh_host *h);
 void akr_bvh_host_free(akr_bvh_host *h);
+/* The 4-wide quantized view the traversal kernels walk (akr_bvh4_node / akr_bvh_leaf), built from
+ * the handle's BVH2 on first call; pointers stay valid until akr_bvh_host_free. */
+int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, uint32_t *root_ref);
+const void *akr_bvh_host_wide_nodes(const akr_bvh_host *h);
+const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h);
 
 int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n);
 int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);

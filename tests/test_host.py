@@ -83,6 +83,78 @@ def test_bvh_degenerate_inputs():
         capi.build_bvh_host(v, np.array([[0, 1, 5000]], np.int32))
 
 
+def _bvh2_leaf_order(nodes, signs):
+    """Leaves of the BVH2 in the reference's depth-first order for a ray direction with these
+    component signs (near child = left iff d[axis] > 0, bvh-accelerator.h:508-514)."""
+    out, stack = [], [int(nodes[0]["child"][0])]
+    while stack:
+        r = stack.pop()
+        if r == 0xFFFFFFFF:
+            continue
+        if r & 0x80000000:
+            out.append(((r & 0x7FFFFFFF) >> 3, (r & 7) + 1))
+            continue
+        nd = nodes[r]
+        c0, c1 = int(nd["child"][0]), int(nd["child"][1])
+        near, far = (c0, c1) if signs[nd["axis"]] else (c1, c0)
+        stack += [far, near]
+    return out
+
+
+def _wide_walk(wide, signs):
+    """Depth-first walk of the wide view with the kernel's slot order; yields (leaf, path boxes)."""
+    wn, lv, root = wide
+    out = []
+
+    def slot_boxes(nd):
+        ex = [(int(nd["meta"]) >> (8 * k)) & 0xFF for k in range(3)]
+        s = [np.float32(2.0 ** (e - 127)) for e in ex]
+        boxes = []
+        for k in range(4):
+            q = [(int(nd["q"][j]) >> (8 * k)) & 0xFF for j in range(6)]
+            lo = [np.float32(np.float32(q[2 * a]) * s[a] + nd["origin"][a]) for a in range(3)]
+            hi = [np.float32(np.float32(q[2 * a + 1]) * s[a] + nd["origin"][a]) for a in range(3)]
+            boxes.append((np.array(lo, np.float32), np.array(hi, np.float32)))
+        return boxes
+
+    def visit(ref, path):
+        if ref == 0xFFFFFFFF:
+            return
+        if ref & 0x80000000:
+            out.append((ref & 0x7FFFFFFF, path))
+            return
+        nd = wn[ref]
+        ax = int(nd["meta"]) >> 24
+        f0, f1, f2 = signs[ax & 3], signs[(ax >> 2) & 3], signs[(ax >> 4) & 3]
+        pa = [0, 1] if f1 else [1, 0]
+        pb = [2, 3] if f2 else [3, 2]
+        boxes = slot_boxes(nd)
+        for k in (pa + pb if f0 else pb + pa):
+            visit(int(nd["child"][k]), path + [boxes[k]])
+
+    visit(root, [])
+    return out
+
+
+@pytest.mark.parametrize("leaf", [1, 4])
+def test_wide_view_invariants(leaf):
+    """The 4-wide traversal view: every leaf's exact box lies inside every quantized slot box on
+    its path (the wide test can only pass more often), leaf records cover the triangles once, and
+    for every direction octant the leaves come in the BVH2 depth-first order."""
+    cs = scene.compile_scene(small_soup(5_000))
+    nodes, tris, info, wide = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, wide=True)
+    wn, lv, root = wide
+    assert sorted((int(l["first"]), int(l["count"])) for l in lv) == sorted(_bvh2_leaf_order(nodes, (1, 1, 1)))
+    for octant in range(8):
+        signs = tuple(bool(octant >> a & 1) for a in range(3))
+        walk = _wide_walk(wide, signs)
+        assert [(int(lv[i]["first"]), int(lv[i]["count"])) for i, _ in walk] == _bvh2_leaf_order(nodes, signs)
+        if octant == 0:
+            for i, path in walk:
+                for lo, hi in path:
+                    assert np.all(lo <= lv[i]["lo"]) and np.all(hi >= lv[i]["hi"])
+
+
 @pytest.mark.parametrize("mk", ["cornell", "soup"])
 def test_oracle_bvh_matches_brute_force(mk):
     sc = cornell() if mk == "cornell" else small_soup(20_000)
