@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=1)
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
+    ap.add_argument("--timed-stats", type=int, default=1,
+                    help="per-kernel HIP events inside the timed region (0: probe their overhead)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -126,6 +128,8 @@ def main():
     cstats = ctx.kernel_stats()
     ctx.set_option("count_tests", 0)
     ctx.reset_stats()
+    if not args.timed_stats:
+        ctx.set_option("stats", 0)
 
     # timed region
     gathered = None
@@ -158,7 +162,12 @@ def main():
         print(json.dumps({"probe": "emulated rank 0 of a tile split", "emulate_world": split, "rank_pixels": npix,
                           "rank_ms_per_step": round(elapsed / K * 1e3, 3),
                           "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3),
-                          "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3)}), flush=True)
+                          "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3),
+                          "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
+                                      for k, v in kstats.items()},
+                          "rays_per_pixel": {"closest": counts["per_mode"]["closest"]["rays"] / max(1, npix),
+                                             "shadow": counts["per_mode"]["shadow"]["rays"] / max(1, npix)}}),
+              flush=True)
         return
     samples = W * H * K
     value = samples / elapsed / 1e6
