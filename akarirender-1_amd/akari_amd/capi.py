@@ -128,6 +128,7 @@ EXPORTS = {
     "akr_bvh_host_nodes": (_P, [_P]),
     "akr_bvh_host_tris": (_P, [_P]),
     "akr_bvh_host_free": (None, [_P]),
+    "akr_hip_render_node": (C.c_int, [C.POINTER(_P), C.c_int32, C.POINTER(PtParams), _P, C.c_int32, _P, _P]),
     "akr_bvh_host_wide": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "akr_bvh_host_wide_nodes": (_P, [_P]),
     "akr_bvh_host_wide_leaves": (_P, [_P]),
@@ -191,6 +192,21 @@ def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost
     if wide:
         return nodes, tris, info, (wn, lv, root.value)
     return nodes, tris, info
+
+
+def render_node(ctxs, spp, max_depth, tiles, width, height, ray_clamp=0.0, exact_cull=False):
+    """akr_hip_render_node: tile j on ctxs[j % len(ctxs)], one host thread per context; returns
+    the full-frame (radiance, weight) accumulated like HipContext.render."""
+    lib = load_library()
+    radiance = np.zeros((height, width, 3), np.float32)
+    weight = np.zeros((height, width), np.float32)
+    arr = (Rect * max(1, len(tiles)))(*[Rect(*t) for t in tiles])
+    hs = (C.c_void_p * len(ctxs))(*[c.h for c in ctxs])
+    p = PtParams(int(spp), int(max_depth), float(ray_clamp), PT_EXACT_CULL if exact_cull else 0)
+    if lib.akr_hip_render_node(hs, len(ctxs), C.byref(p), C.cast(arr, C.c_void_p), len(tiles), _ptr(radiance),
+                               _ptr(weight)) != 0:
+        raise AkrError(lib.akr_hip_last_error(ctxs[0].h).decode() if ctxs else "no contexts")
+    return radiance, weight
 
 
 def _ptr(a: np.ndarray):

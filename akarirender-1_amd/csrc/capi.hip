@@ -15,6 +15,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "akr_device.h"
@@ -803,6 +804,56 @@ int akr_hip_trace_device(akr_hip_ctx *ctx, const void *d_rays, uint64_t n, void 
         hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
         ctx->trace(reinterpret_cast<const float4 *>(d_rays), n, reinterpret_cast<akr_hit *>(d_hits), any_hit, st);
     });
+}
+
+int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_params *params, const akr_rect *tiles,
+                        int32_t n_tiles, float *radiance, float *weight) {
+    if (!ctxs || n_ctx < 1) return -1;
+    for (int32_t k = 0; k < n_ctx; k++)
+        if (!ctxs[k]) return -1;
+    akr_hip_ctx *lead = ctxs[0];
+    if (!params || !radiance || !weight || n_tiles < 0 || (n_tiles > 0 && !tiles)) {
+        lead->err = "null or invalid argument";
+        return -1;
+    }
+    // tile j -> context j % n_ctx (interleaved, like the multi-process split of akari_amd/dist.py);
+    // one host thread per context, each bound to its device by guard()
+    std::vector<std::vector<akr_rect>> part(n_ctx);
+    for (int32_t j = 0; j < n_tiles; j++) part[j % n_ctx].push_back(tiles[j]);
+    std::vector<std::vector<float4>> film(n_ctx);
+    std::vector<std::vector<uint32_t>> pix(n_ctx);
+    std::vector<int> status(n_ctx, 0);
+    std::vector<std::thread> th;
+    for (int32_t k = 0; k < n_ctx; k++) {
+        th.emplace_back([&, k] {
+            akr_hip_ctx *c = ctxs[k];
+            status[k] = guard(c, [&] {
+                hipStream_t st = c->stream;
+                const uint64_t N = c->render(*params, part[k].data(), (int32_t)part[k].size(), st);
+                film[k].resize(N);
+                if (N) HIPCHK(hipMemcpyAsync(film[k].data(), c->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                pix[k] = c->h_pixel;
+            });
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int32_t k = 0; k < n_ctx; k++)
+        if (status[k] != 0) {
+            if (k) lead->err = "context " + std::to_string(k) + ": " + ctxs[k]->err;
+            return -1;
+        }
+    const int W = lead->cam.width;
+    for (int32_t k = 0; k < n_ctx; k++)  // Film::merge_tile (core/film.h:85-95), in context order
+        for (size_t i = 0; i < film[k].size(); i++) {
+            const uint32_t px = pix[k][i];
+            const uint64_t p = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
+            radiance[3 * p + 0] += film[k][i].x;
+            radiance[3 * p + 1] += film[k][i].y;
+            radiance[3 * p + 2] += film[k][i].z;
+            weight[p] += film[k][i].w;
+        }
+    return 0;
 }
 
 int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles, int32_t n_tiles,

@@ -190,6 +190,14 @@ int akr_hip_trace_device(akr_hip_ctx *ctx, const void *d_rays, uint64_t n, void 
  * Film's Pixel{radiance, weight} (core/film.h:31-35).  Synchronous. */
 int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles,
                    int32_t n_tiles, float *radiance, float *weight);
+/* Multi-GPU render from one host process (SURVEY.md §8b akr_hip_render_node): tile j goes to
+ * ctxs[j % n_ctx] (one context per device, each holding the same scene and camera), the contexts
+ * render concurrently on one host thread each, and their films are merged into the host buffers
+ * in context order — the same pixels as akr_hip_render on one context, bit for bit.
+ * (Multi-process runs over RCCL use akr_hip_render_device + akari_amd/dist.py instead.)
+ * On failure the message is on ctxs[0]. */
+int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_params *params,
+                        const akr_rect *tiles, int32_t n_tiles, float *radiance, float *weight);
 /* Same, but writes (overwrites) device buffers in packed tile order: pixel k of the tile list
  * (tiles in order, row-major inside a tile) -> radiance[3k..3k+2], weight[k].  Returns the
  * pixel count in *n_pixels.  Asynchronous on `stream`. */

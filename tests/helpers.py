@@ -55,6 +55,24 @@ def mixed_scene(resolution=(48, 48)):
     return sc
 
 
+def textured_scene(resolution=(48, 48)):
+    """Cornell geometry with image textures on diffuse, glossy roughness, mix fraction and emitter
+    colour (a15); texcoords stretched to [-1, 2] so the fmod wrap and the clamp are exercised."""
+    sc = mixed_scene(resolution)
+    m = sc.shapes[0]
+    rng = np.random.default_rng(11)
+    img = lambda h, w: scene.ImageTexture(rng.random((h, w, 4), dtype=np.float32))
+    m.texcoords = (np.asarray(m.texcoords, np.float32) * np.float32(3.0) - np.float32(1.0)).astype(np.float32)
+    ct = scene.ConstantTexture
+    m.materials[0] = scene.DiffuseMaterial(img(23, 37))                       # floor
+    m.materials[2] = scene.GlossyMaterial(img(5, 7), img(9, 4))               # back wall: roughness image
+    m.materials[6] = scene.MixMaterial(img(16, 16), scene.DiffuseMaterial(img(3, 3)),
+                                       scene.GlossyMaterial(ct([0.8, 0.8, 0.8]), ct([0.3, 0.3, 0.3])))
+    m.materials[7] = scene.EmissiveMaterial(scene.ImageTexture(rng.random((4, 6, 4), dtype=np.float32) * 20),
+                                            double_sided=False)
+    return sc
+
+
 def hits_to_gid(hits, mesh_base):
     gid = np.full(hits.shape[0], 0xFFFFFFFF, np.uint32)
     ok = hits["geom_id"] >= 0

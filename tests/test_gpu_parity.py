@@ -10,7 +10,7 @@ import pytest
 
 import py_oracle
 from akari_amd import capi, scene
-from helpers import cornell, edge_rays, hits_to_gid, mixed_scene, random_rays, small_soup
+from helpers import cornell, edge_rays, hits_to_gid, mixed_scene, random_rays, small_soup, textured_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -168,6 +168,31 @@ def test_render_glossy_mix_bit_exact(hip_ctx_factory):
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, mixed_scene((48, 48)))
         _check_render(ctx, orc, 8, 5, [(0, 0, 48, 48)], 48, 48)
+
+
+def test_render_image_textures_bit_exact(hip_ctx_factory):
+    """ImageTexture (texture.h:39-57, View lookup image.hpp:83-99) on diffuse colour, glossy
+    roughness, mix fraction and emission, with texcoords outside [0, 1]."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, textured_scene((40, 40)))
+        assert len(cs.images) == 6
+        rad, w = _check_render(ctx, orc, 6, 5, [(0, 0, 40, 40)], 40, 40)
+        assert rad.mean() > 0
+
+
+def test_render_node_matches_single_context(hip_ctx_factory):
+    """akr_hip_render_node (two contexts on device 0 here; one per GPU in production) splits the
+    tiles between contexts and gives the single-context image bit for bit."""
+    with hip_ctx_factory(0) as a, hip_ctx_factory(0) as b:
+        sc = cornell((48, 32))
+        cs, orc = _setup(a, sc)
+        scene.upload_scene(b, cs)
+        tiles = [(x, y, x + 16, y + 16) for y in range(0, 32, 16) for x in range(0, 48, 16)]
+        ref, wref = a.render(4, 5, tiles, 48, 32)
+        rad, w = capi.render_node([a, b], 4, 5, tiles, 48, 32)
+        assert np.array_equal(w, wref) and np.array_equal(rad, ref)
+        orad, ow, _ = orc.render(4, 5, tiles=tiles)
+        assert np.array_equal(rad, orad)
 
 
 def test_render_device_packed(hip_ctx_factory):
