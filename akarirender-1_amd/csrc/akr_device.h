@@ -37,8 +37,7 @@ constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this
 constexpr uint32_t kWorkShards = AKR_WORK_SHARDS;  // dynamic-fetch counters per trace launch (>= one per XCD)
 constexpr uint32_t kWorkStride = 32;  // u32 between counters: each on its own 128-B line
 constexpr uint32_t kWorkWords = kWorkShards * kWorkStride;
-// per trace: wide-kernel fetch counters, set-aside (slow) count, BVH2-kernel fetch counters
-constexpr uint32_t kTraceWords = 2 * kWorkWords + kWorkStride;
+constexpr uint32_t kTraceWords = kWorkWords;  // per trace launch
 
 // First queue index of shard k of [0, n) (k = kWorkShards gives n).
 __host__ __device__ inline uint32_t shard_begin(uint32_t n, uint32_t k) {
@@ -107,9 +106,6 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     const float4 *wide_nodes;      // akr_bvh4_node as 4 x float4
     const float4 *wide_leaves;     // akr_bvh_leaf as 2 x float4
     uint32_t wide_root;            // wide reference of the real root
-    const uint32_t *ray_index;     // optional indirection: queue entry -> ray index (BVH2 slow path)
-    uint32_t *slow_idx;            // wide kernel: rays that need the exact-NaN BVH2 path
-    uint32_t *slow_count;
     TraceCounters *counters;       // [3]: closest, any, shadow
 };
 

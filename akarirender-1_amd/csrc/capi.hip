@@ -186,7 +186,6 @@ struct akr_hip_ctx {
     hipEvent_t ev_fork = nullptr, ev_shade[2] = {nullptr, nullptr}, ev_shadow[2] = {nullptr, nullptr};
     DBuf<uint2> d_ovf, d_ovf_side;  // traversal stack overflow: main-stream and side-stream traces
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
-    DBuf<uint32_t> d_slow[2];  // rays the wide kernel hands to the BVH2 kernel (main, side stream)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     DBuf<float4> d_trace_rays;
@@ -408,30 +407,16 @@ struct akr_hip_ctx {
         for (int k = 0; k < 2; k++) {
             d_sray[k].reserve(2 * n);
             d_scolor[k].reserve(n);
-            d_slow[k].reserve(n);
         }
         d_L.reserve(n);
         d_film.reserve(n);
         cap = n;
     }
 
-    // One trace: the wide kernel over the queue, then the BVH2 kernel over the (usually empty)
-    // list of rays the wide kernel set aside because their slab values could be NaN.  `t.work`
-    // is a kTraceWords area: wide fetch counters, the set-aside count, BVH2 fetch counters.
-    void trace_launch(int mode, bool tight, const TraceArgs &t, uint64_t n_max, uint32_t *slow, hipStream_t st) {
-        if (!wide) {
-            launch_trace(mode, count, tight, false, t, grid_for(mode, n_max), st);
-            return;
-        }
-        TraceArgs w = t;
-        w.slow_idx = slow;
-        w.slow_count = t.work + kWorkWords;
-        launch_trace(mode, count, tight, true, w, grid_for(mode, n_max), st);
-        TraceArgs s = t;
-        s.work = t.work + kWorkWords + kWorkStride;
-        s.count = w.slow_count;
-        s.ray_index = slow;
-        launch_trace(mode, count, tight, false, s, std::min<uint32_t>(grid_for(mode, n_max), 4 * (uint32_t)n_cu), st);
+    // One trace launch: the 4-wide kernel (which traces its rare NaN-prone rays inline with the
+    // exact BVH2 walk), or the BVH2 kernel when the "wide" option is off.
+    void trace_launch(int mode, bool tight, const TraceArgs &t, uint64_t n_max, hipStream_t st) {
+        launch_trace(mode, count, tight, wide, t, grid_for(mode, n_max), st);
     }
 
     TraceArgs trace_args(uint32_t *work) {
@@ -466,13 +451,12 @@ struct akr_hip_ctx {
         require_ready();
         if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
         HIPCHK(hipMemsetAsync(d_work.p, 0, kTraceWords * sizeof(uint32_t), st));
-        d_slow[0].reserve(n);
         TraceArgs t = trace_args(d_work.p);
         t.rays = rays;
         t.n = (uint32_t)n;
         t.abi_hits = hits;
         int mode = any ? TRACE_ANY : TRACE_CLOSEST;
-        timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, d_slow[0].p, st); });
+        timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, st); });
         HIPCHK(hipGetLastError());
     }
 
@@ -530,7 +514,7 @@ struct akr_hip_ctx {
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
-                timed("trace_closest", st, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, d_slow[0].p, st); });
+                timed("trace_closest", st, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, st); });
                 // shade(b) refills shadow queue b % 2: the shadow trace of bounce b - 2 must be done
                 if (b >= 2) HIPCHK(hipStreamWaitEvent(st, ev_shadow[odd], 0));
                 ShadeArgs sh{};
@@ -562,7 +546,7 @@ struct akr_hip_ctx {
                     ts.count = scount(b);
                     ts.shadow_color = d_scolor[odd].p;
                     ts.L = d_L.p;
-                    timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, d_slow[1].p, side); });
+                    timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, side); });
                     HIPCHK(hipEventRecord(ev_shadow[odd], side));
                 }
             }

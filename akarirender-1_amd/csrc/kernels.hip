@@ -275,6 +275,94 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
     return tested;
 }
 
+// Result of one finished ray: the closest hit (float4 queue record or akr_hit), or for a shadow
+// ray the NEE contribution L[slot] += colour when unoccluded (a slot has at most one shadow ray
+// per bounce, so there is no write race).
+template <int MODE>
+__device__ __forceinline__ void emit_result(const TraceArgs &a, uint32_t idx, float best, float bu, float bv,
+                                            uint32_t bgid, bool occluded) {
+    constexpr bool ANY = MODE != TRACE_CLOSEST;
+    if (MODE == TRACE_SHADOW) {
+        if (!occluded) {
+            const float4 c = a.shadow_color[idx];
+            const uint32_t slot = fbits(c.w);
+            float4 l = a.L[slot];
+            l.x += c.x;
+            l.y += c.y;
+            l.z += c.z;
+            a.L[slot] = l;
+        }
+    } else if (a.abi_hits) {
+        akr_hit h;
+        const bool hit = ANY ? occluded : (bgid != kNoHit);
+        h.t = hit ? best : kInf;
+        h.u = hit ? bu : 0.0f;
+        h.v = hit ? bv : 0.0f;
+        h.geom_id = -1;
+        h.prim_id = -1;
+        if (hit) {
+            int lo = 0, hi = a.n_meshes;  // largest m with mesh_base[m] <= gid
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) / 2;
+                if (a.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
+            }
+            h.geom_id = lo;
+            h.prim_id = (int32_t)(bgid - a.mesh_base[lo]);
+        }
+        h._pad[0] = h._pad[1] = h._pad[2] = 0;
+        a.abi_hits[idx] = h;
+    } else {
+        a.hits[idx] = make_float4(best, bu, bv, bitsf(bgid));
+    }
+}
+
+// Exact BVH2 traversal of one lane's ray to completion (reference order and NaN semantics), for
+// the rare rays the wide kernel cannot take (fast_box_ok false: a zero or denormal direction
+// component, a non-finite origin or a NaN interval).  Runs inline while the rest of the wave
+// waits, so no extra launch is ever needed; the lane's LDS stack is free (it holds no ray).
+template <int MODE, bool TIGHT>
+__device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t idx, V3 o, V3 d, V3 invd, float tmin,
+                                              float tmax, lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid) {
+    constexpr bool ANY = MODE != TRACE_CLOSEST;
+    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
+    const uint4 *nodesu = reinterpret_cast<const uint4 *>(a.nodes);
+    const float4 r0 = nodesf[0], r2 = nodesf[2];
+    const uint32_t root = nodesu[3].x;
+    float best = kInf, bu = 0.0f, bv = 0.0f;
+    uint32_t bgid = kNoHit;
+    bool occluded = false;
+    int sp = 0;
+    const float tr = box_test<TIGHT, false>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+    uint32_t cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
+    while (cur != AKR_CHILD_EMPTY) {
+        if (is_internal(cur)) {
+            visit_node<TIGHT, false, ANY>(nodesf, nodesu, cur, o, d, invd, tmin, tmax, best, s_stack, ovf, a.ovf_threads,
+                                          tid, gtid, sp);
+            continue;
+        }
+        const uint32_t first = akr_leaf_first(cur), cnt = akr_leaf_count(cur);
+        for (uint32_t k = 0; k < cnt; k++) {
+            const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
+            const float4 tb = a.tris[3 * (size_t)(first + k) + 1];
+            const float4 tc = a.tris[3 * (size_t)(first + k) + 2];
+            float t, u, v;
+            if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
+                best = t;
+                bu = u;
+                bv = v;
+                bgid = fbits(ta.w);
+                if (ANY) {
+                    occluded = true;
+                    break;
+                }
+            }
+        }
+        if (ANY && occluded) break;
+        cur = stack_pop(s_stack, ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
+    }
+    emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
+}
+
 // One ray per lane; persistent waves.  Per outer iteration a wave
 //   1. refills idle lanes from the queue (one atomic; the new rays' loads overlap step 2),
 //   2. runs the traversal phase: visit internal nodes until every busy lane holds a pending leaf
@@ -286,11 +374,12 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
 // box tests but never a different hit.  A node's two child boxes are tested when the node is
 // visited and the far child is pushed with its entry distance, re-compared against the current
 // best when popped — the reference's pop-time test of the node's own box.
-#ifdef AKR_TRACE_WAVES  // tuning variants: cap registers for this many waves per SIMD
-#define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
-#else
-#define AKR_TRACE_ATTR
+// Registers are capped for 6 waves per SIMD (<= 80 VGPRs), which the LDS stack allows anyway
+// (6 x 24 KB workgroups per CU); uncapped, the inlined exact-lane path pushes the kernel to 85.
+#ifndef AKR_TRACE_WAVES
+#define AKR_TRACE_WAVES 6
 #endif
+#define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
 template <int MODE, bool COUNT, bool TIGHT, bool WIDE>
 __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
@@ -338,9 +427,9 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 if (!busy) {
                     const uint32_t my = first + lane_prefix(idle);
                     if (my < s_hi && base < s_hi - s_lo) {
-                        idx = a.ray_index ? a.ray_index[my] : my;
-                        ra = a.rays[2 * (size_t)idx];
-                        rb = a.rays[2 * (size_t)idx + 1];
+                        idx = my;
+                        ra = a.rays[2 * (size_t)my];
+                        rb = a.rays[2 * (size_t)my + 1];
                         fresh = true;
                     }
                 }
@@ -439,38 +528,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             }
             if (busy && ((ANY && occluded) || cur == AKR_CHILD_EMPTY)) {
                 busy = false;
-                if (MODE == TRACE_SHADOW) {
-                    if (!occluded) {
-                        const float4 c = a.shadow_color[idx];
-                        const uint32_t slot = fbits(c.w);
-                        float4 l = a.L[slot];
-                        l.x += c.x;
-                        l.y += c.y;
-                        l.z += c.z;
-                        a.L[slot] = l;
-                    }
-                } else if (a.abi_hits) {
-                    akr_hit h;
-                    const bool hit = ANY ? occluded : (bgid != kNoHit);
-                    h.t = hit ? best : kInf;
-                    h.u = hit ? bu : 0.0f;
-                    h.v = hit ? bv : 0.0f;
-                    h.geom_id = -1;
-                    h.prim_id = -1;
-                    if (hit) {
-                        int lo = 0, hi = a.n_meshes;  // largest m with mesh_base[m] <= gid
-                        while (hi - lo > 1) {
-                            const int mid = (lo + hi) / 2;
-                            if (a.mesh_base[mid] <= bgid) lo = mid; else hi = mid;
-                        }
-                        h.geom_id = lo;
-                        h.prim_id = (int32_t)(bgid - a.mesh_base[lo]);
-                    }
-                    h._pad[0] = h._pad[1] = h._pad[2] = 0;
-                    a.abi_hits[idx] = h;
-                } else {
-                    a.hits[idx] = make_float4(best, bu, bv, bitsf(bgid));
-                }
+                emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
             }
         }
         if (fresh) {
@@ -479,8 +537,9 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             tmin = ra.w;
             tmax = rb.w;
             invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            if (WIDE && !fast_box_ok(o, invd, tmin, tmax)) {  // rare: the BVH2 kernel traces it
-                a.slow_idx[atomicAdd(a.slow_count, 1u)] = idx;
+            if (WIDE && !fast_box_ok(o, invd, tmin, tmax)) {  // rare: exact BVH2 traversal, inline
+                if (COUNT) c_rays++;
+                trace_exact_lane<MODE, TIGHT>(a, idx, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid);
                 fresh = false;
             }
         }

@@ -26,7 +26,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic bytes per ray / AABB / triangle test
 
 
-TRACE_KERNEL_PROF_NAME = "k_trace<0, false, true>"   # closest hit, uncounted, tight cull (rocprof name)
+TRACE_KERNEL_PROF_NAME = "k_trace<0, false, true, true>"   # closest hit, uncounted, tight cull, wide (rocprof name)
 
 
 def log(*a):
