@@ -158,7 +158,7 @@ def device_count() -> int:
     return n.value
 
 
-def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=1.0,
+def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0,
                    n_threads=0, wide=False):
     """Run the product BVH builder on the host (no device): returns (nodes, tris, info), plus
     (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide`."""
@@ -289,7 +289,7 @@ class HipContext:
         pw = np.ascontiguousarray(power, np.float32)
         self._check(self.lib.akr_hip_upload_lights(self.h, C.cast(arr, C.c_void_p), len(lights), _ptr(pw)))
 
-    def build_accel(self, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=1.0, n_threads=0):
+    def build_accel(self, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0, n_threads=0):
         p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads)
         self._check(self.lib.akr_hip_build_accel(self.h, C.byref(p)))
         return self.accel_info()

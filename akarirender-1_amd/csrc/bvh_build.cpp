@@ -80,7 +80,7 @@ class Builder {
         bins_ = std::clamp(p.n_bins > 0 ? p.n_bins : 32, 2, kMaxBins);
         max_leaf_ = std::clamp(p.max_leaf_size > 0 ? p.max_leaf_size : 4, 1, AKR_LEAF_MAX);
         ct_ = p.traversal_cost > 0 ? p.traversal_cost : 1.0f;
-        ci_ = p.intersect_cost > 0 ? p.intersect_cost : 1.0f;
+        ci_ = p.intersect_cost > 0 ? p.intersect_cost : 4.0f;
     }
 
     void run(BvhOutput &out) {

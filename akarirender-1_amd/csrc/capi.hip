@@ -719,7 +719,7 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         p.max_leaf_size = 4;
         p.n_bins = 32;
         p.traversal_cost = 1.0f;
-        p.intersect_cost = 1.0f;
+        p.intersect_cost = 4.0f;
         if (params) p = *params;
         BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
         build_bvh(in, p, ctx->bvh);
@@ -891,7 +891,7 @@ int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t
         p.max_leaf_size = 4;
         p.n_bins = 32;
         p.traversal_cost = 1.0f;
-        p.intersect_cost = 1.0f;
+        p.intersect_cost = 4.0f;
         if (params) p = *params;
         std::unique_ptr<akr_bvh_host> h(new akr_bvh_host());
         BvhInput in{vertices, indices, n_triangles};

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--leaf", type=int, default=4)
+    ap.add_argument("--sah-isect", type=float, default=4.0, help="SAH triangle-test cost (traversal step = 1)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
@@ -97,7 +98,8 @@ def main():
     cs = scene.compile_scene(sc)
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
-    info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, n_threads=min(16, os.cpu_count() or 1))
+    info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect,
+                              n_threads=min(16, os.cpu_count() or 1))
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)
@@ -180,7 +182,8 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     sh = counts["per_mode"]["shadow"]
     traffic, traffic_src = measured_traffic(TRACE_KERNEL_PROF_NAME, {
-        "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf})
+        "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf,
+        "sah_isect": args.sah_isect})
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
@@ -225,7 +228,8 @@ def main():
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)", "triangles": cs.n_tris,
                    "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
-                   "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf},
+                   "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
+                   "sah_isect": args.sah_isect},
         "roofline": roofline, "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                     for k, v in kstats.items()},
