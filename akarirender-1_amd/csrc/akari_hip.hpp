@@ -17,6 +17,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <stdexcept>
+#include <cmath>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -118,6 +120,85 @@ struct Film {
         float w = weight[p];
         for (int c = 0; c < 3; c++) rgb[c] = w != 0 ? radiance[3 * p + c] / w : radiance[3 * p + c];
     }
+    // Film::write_image (core/film.h:97-113) with GammaCorrection (common/color.h:58-61) and the
+    // 8-bit quantisation of DefaultImageWriter (core/image.cpp:38-60): row-major RGB bytes.  pow
+    // in f64 rounded to f32 (the correctly rounded powf); identical to akari_amd/film.py.
+    std::vector<uint8_t> srgb8() const {
+        std::vector<uint8_t> out(3 * (size_t)width * height);
+        for (int y = 0; y < height; y++)
+            for (int x = 0; x < width; x++) {
+                float rgb[3];
+                pixel(x, y, rgb);
+                for (int c = 0; c < 3; c++) {
+                    const float L = rgb[c];
+                    const float p = (float)std::pow((double)L, (double)(1.0f / 2.4f));
+                    float s = L < 0.0031308f ? L * 12.92f : 1.055f * p - 0.055f;
+                    if (!(s >= 0.0f)) s = 0.0f;  // clamp to [0, 1] (NaN -> 0)
+                    if (s > 1.0f) s = 1.0f;
+                    const int q = (int)std::round((double)s * 255.5);
+                    out[3 * ((size_t)x + (size_t)y * width) + c] = (uint8_t)std::min(255, std::max(0, q));
+                }
+            }
+        return out;
+    }
+    // 8-bit RGB PNG with stored (uncompressed) deflate blocks: no codec dependency.
+    bool write_png(const std::string &path) const {
+        const std::vector<uint8_t> rgb = srgb8();
+        std::vector<uint8_t> raw;
+        raw.reserve((size_t)height * (1 + 3 * (size_t)width));
+        for (int y = 0; y < height; y++) {
+            raw.push_back(0);  // filter type 0
+            raw.insert(raw.end(), rgb.begin() + 3 * (size_t)y * width, rgb.begin() + 3 * (size_t)(y + 1) * width);
+        }
+        std::vector<uint8_t> z = {0x78, 0x01};
+        for (size_t pos = 0; pos < raw.size() || pos == 0;) {
+            const size_t n = std::min<size_t>(65535, raw.size() - pos);
+            const bool last = pos + n >= raw.size();
+            z.push_back(last ? 1 : 0);
+            z.push_back((uint8_t)(n & 0xFF));
+            z.push_back((uint8_t)(n >> 8));
+            z.push_back((uint8_t)(~n & 0xFF));
+            z.push_back((uint8_t)((~n >> 8) & 0xFF));
+            z.insert(z.end(), raw.begin() + pos, raw.begin() + pos + n);
+            pos += n;
+            if (last) break;
+        }
+        uint32_t a = 1, b = 0;  // Adler-32 of the raw stream
+        for (uint8_t c : raw) {
+            a = (a + c) % 65521;
+            b = (b + a) % 65521;
+        }
+        for (int k = 3; k >= 0; k--) z.push_back((uint8_t)(((b << 16) | a) >> (8 * k)));
+        FILE *f = std::fopen(path.c_str(), "wb");
+        if (!f) return false;
+        static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+        std::fwrite(sig, 1, 8, f);
+        auto be32 = [](std::vector<uint8_t> &v, uint32_t x) {
+            for (int k = 3; k >= 0; k--) v.push_back((uint8_t)(x >> (8 * k)));
+        };
+        auto chunk = [&](const char *tag, const std::vector<uint8_t> &data) {
+            std::vector<uint8_t> c;
+            be32(c, (uint32_t)data.size());
+            c.insert(c.end(), tag, tag + 4);
+            c.insert(c.end(), data.begin(), data.end());
+            uint32_t crc = 0xFFFFFFFFu;  // CRC-32 over tag + data
+            for (size_t i = 4; i < c.size(); i++) {
+                crc ^= c[i];
+                for (int k = 0; k < 8; k++) crc = (crc >> 1) ^ (0xEDB88320u & (0u - (crc & 1u)));
+            }
+            be32(c, crc ^ 0xFFFFFFFFu);
+            std::fwrite(c.data(), 1, c.size(), f);
+        };
+        std::vector<uint8_t> ihdr;
+        be32(ihdr, (uint32_t)width);
+        be32(ihdr, (uint32_t)height);
+        ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});
+        chunk("IHDR", ihdr);
+        chunk("IDAT", z);
+        chunk("IEND", {});
+        std::fclose(f);
+        return true;
+    }
     // Portable float map (no image codec dependency); write_image's divide-by-weight applied.
     bool write_pfm(const std::string &path) const {
         FILE *f = std::fopen(path.c_str(), "wb");
@@ -153,6 +234,22 @@ class HipPathTracer {
               akr_hip_render(scene.handle(), &p, tiles.data(), (int32_t)tiles.size(), film.radiance.data(),
                              film.weight.data()),
               "render");
+    }
+
+    // Multi-GPU in one process (akr_hip_render_node): tile j on accelerators[j % n], one per device,
+    // each built from the same scene; the merged film equals render() on one of them.
+    void render_node(const std::vector<const HipAccelerator *> &accels, Film &film) const {
+        if (accels.empty()) throw std::runtime_error("render_node: no accelerators");
+        std::vector<akr_rect> tiles;
+        for (int y = 0; y < film.height; y += tile_size)
+            for (int x = 0; x < film.width; x += tile_size) tiles.push_back({x, y, x + tile_size, y + tile_size});
+        std::vector<akr_hip_ctx *> h;
+        for (auto *a : accels) h.push_back(a->handle());
+        akr_pt_params p{spp, max_depth, ray_clamp, 0};
+        check(h[0],
+              akr_hip_render_node(h.data(), (int32_t)h.size(), &p, tiles.data(), (int32_t)tiles.size(),
+                                  film.radiance.data(), film.weight.data()),
+              "render_node");
     }
 };
 

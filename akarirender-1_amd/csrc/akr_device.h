@@ -104,7 +104,8 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     float4 *L;                     //   L[slot] += colour when unoccluded
     uint2 *stack_ovf;              // (ref, t bits) entries beyond the LDS stack
     const float4 *wide_nodes;      // akr_bvh4_node as 4 x float4
-    const float4 *wide_leaves;     // akr_bvh_leaf as 2 x float4
+    const float4 *wide_leaves;     // leaf blob: per leaf [lo.xyz hi.x | hi.yz first count] + its triangles
+                                   // (3 x float4 each); wide leaf refs hold the float4 offset
     uint32_t wide_root;            // wide reference of the real root
     TraceCounters *counters;       // [3]: closest, any, shadow
 };

@@ -157,7 +157,8 @@ struct akr_hip_ctx {
     // device scene
     DBuf<akr_bvh_node> d_nodes;
     DBuf<akr_bvh4_node> d_wnodes;
-    DBuf<akr_bvh_leaf> d_wleaves;
+    DBuf<float4> d_wleaves;          // leaf blob (see TraceArgs::wide_leaves)
+    uint32_t wide_root_dev = AKR_CHILD_EMPTY;
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
@@ -424,7 +425,7 @@ struct akr_hip_ctx {
         t.nodes = d_nodes.p;
         t.wide_nodes = reinterpret_cast<const float4 *>(d_wnodes.p);
         t.wide_leaves = reinterpret_cast<const float4 *>(d_wleaves.p);
-        t.wide_root = bvh4.root_ref;
+        t.wide_root = wide_root_dev;
         t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
@@ -726,10 +727,41 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         auto &b = ctx->bvh;
         build_bvh4(b.nodes, ctx->bvh4);
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
+        // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
+        // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the
+        // wide nodes become float4 offsets into the blob.
+        std::vector<uint32_t> leaf_off(ctx->bvh4.leaves.size());
+        std::vector<float4> blob;
+        size_t words = 0;
+        for (const auto &l : ctx->bvh4.leaves) words += 2 + 3 * (size_t)l.count;
+        if (words >= AKR_CHILD_LEAF) throw std::runtime_error("BVH too large for the wide leaf blob");
+        blob.reserve(words);
+        const float4 *tri4 = reinterpret_cast<const float4 *>(b.tris.data());
+        for (size_t i = 0; i < ctx->bvh4.leaves.size(); i++) {
+            const akr_bvh_leaf &l = ctx->bvh4.leaves[i];
+            leaf_off[i] = (uint32_t)blob.size();
+            float4 h0, h1;
+            h0.x = l.lo[0], h0.y = l.lo[1], h0.z = l.lo[2], h0.w = l.hi[0];
+            uint32_t fc[2] = {l.first, l.count};
+            h1.x = l.hi[1], h1.y = l.hi[2];
+            std::memcpy(&h1.z, &fc[0], 4);
+            std::memcpy(&h1.w, &fc[1], 4);
+            blob.push_back(h0);
+            blob.push_back(h1);
+            for (uint32_t k = 0; k < 3 * l.count; k++) blob.push_back(tri4[3 * (size_t)l.first + k]);
+        }
+        auto remap = [&](uint32_t r) {
+            return (r != AKR_CHILD_EMPTY && (r & AKR_CHILD_LEAF)) ? (AKR_CHILD_LEAF | leaf_off[r & 0x7FFFFFFFu]) : r;
+        };
+        std::vector<akr_bvh4_node> wn = ctx->bvh4.nodes;
+        for (auto &n : wn)
+            for (auto &c : n.child) c = remap(c);
+        ctx->wide_root_dev = remap(ctx->bvh4.root_ref);
         ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
         ctx->d_wleaves.reserve(1);
-        ctx->d_wnodes.upload(ctx->bvh4.nodes.data(), ctx->bvh4.nodes.size(), ctx->stream);
-        ctx->d_wleaves.upload(ctx->bvh4.leaves.data(), ctx->bvh4.leaves.size(), ctx->stream);
+        ctx->d_wnodes.upload(wn.data(), wn.size(), ctx->stream);
+        ctx->d_wleaves.upload(blob.data(), blob.size(), ctx->stream);
+        HIPCHK(hipStreamSynchronize(ctx->stream));  // before the host staging vectors go away
         ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));
         ctx->info.n_nodes = b.nodes.size();

@@ -493,24 +493,32 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             }
             // ---- 3. leaf phase
             if (busy && leaf != AKR_CHILD_EMPTY) {
-                uint32_t first, cnt;
+                uint32_t cnt;
+                const float4 *tp;  // this leaf's triangle records (3 x float4 each)
+                float4 pa, pb, pc;  // the first one, fetched together with the leaf header
                 if (WIDE) {  // the leaf's exact box, with the current best: the BVH2 pop-time test
-                    const float4 *lr = a.wide_leaves + 2 * (size_t)(leaf & 0x7FFFFFFFu);
+                    const float4 *lr = a.wide_leaves + (leaf & 0x7FFFFFFFu);
                     const float4 l0 = lr[0], l1 = lr[1];  // lo.xyz hi.x | hi.yz first count
+                    pa = lr[2];
+                    pb = lr[3];
+                    pc = lr[4];
                     const float tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
                     const bool in = !(tl < 0.0f || tl > (ANY ? tmax : best));
                     if (COUNT) c_box++;
-                    first = fbits(l1.z);
                     cnt = in ? fbits(l1.w) : 0u;
+                    tp = lr + 2;
                 } else {
-                    first = akr_leaf_first(leaf);
+                    tp = a.tris + 3 * (size_t)akr_leaf_first(leaf);
                     cnt = akr_leaf_count(leaf);
+                    pa = tp[0];
+                    pb = tp[1];
+                    pc = tp[2];
                 }
                 for (uint32_t k = 0; k < cnt; k++) {
                     if (COUNT && lane_prefix(__ballot(1)) == 0) c_stri += 64;
-                    const float4 ta = a.tris[3 * (size_t)(first + k) + 0];
-                    const float4 tb = a.tris[3 * (size_t)(first + k) + 1];
-                    const float4 tc = a.tris[3 * (size_t)(first + k) + 2];
+                    const float4 ta = k == 0 ? pa : tp[3 * k + 0];
+                    const float4 tb = k == 0 ? pb : tp[3 * k + 1];
+                    const float4 tc = k == 0 ? pc : tp[3 * k + 2];
                     if (COUNT) c_tri++;
                     float t, u, v;
                     if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
