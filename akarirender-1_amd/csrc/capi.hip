@@ -179,12 +179,17 @@ struct akr_hip_ctx {
     size_t cap = 0;
     std::vector<uint32_t> h_pixel;
     DBuf<uint32_t> d_pixel, d_seed, d_slot0, d_slot1, d_counts;
-    DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_L, d_film;
+    DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_film;
+    DBuf<float4> d_L[2];  // per-sample radiance, alternating by sample pass (passes overlap)
     DBuf<float4> d_sray[2], d_scolor[2];  // shadow queues, alternating by bounce
     // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
     // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_shade[2] = {nullptr, nullptr}, ev_shadow[2] = {nullptr, nullptr};
+    // Both internal: `main` (high priority) runs raygen / closest-hit / shade, `side` (low priority)
+    // runs shadow traces and splat, so the last shadow trace and splat of sample pass s overlap
+    // raygen and the first closest-hit trace of pass s + 1.
+    hipStream_t main_st = nullptr, side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_shade[2] = {nullptr, nullptr},
+               ev_shadow[2] = {nullptr, nullptr}, ev_splat[2] = {nullptr, nullptr};
     DBuf<uint2> d_ovf, d_ovf_side;  // traversal stack overflow: main-stream and side-stream traces
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
     uint32_t ovf_threads = 0;
@@ -215,8 +220,10 @@ struct akr_hip_ctx {
         }
         for (auto e : pool) (void)hipEventDestroy(e);
         if (side) (void)hipStreamSynchronize(side);
-        for (hipEvent_t e : {ev_fork, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1]})
+        if (main_st) (void)hipStreamSynchronize(main_st);
+        for (hipEvent_t e : {ev_fork, ev_join, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1]})
             if (e) (void)hipEventDestroy(e);
+        if (main_st) (void)hipStreamDestroy(main_st);
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -383,8 +390,11 @@ struct akr_hip_ctx {
 
     void ensure_side_stream() {
         if (side) return;
-        HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-        for (hipEvent_t *e : {&ev_fork, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1]})
+        int least = 0, greatest = 0;  // numerically lower = higher priority
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(hipStreamCreateWithPriority(&main_st, hipStreamNonBlocking, greatest));
+        HIPCHK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, least));
+        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
 
@@ -409,7 +419,8 @@ struct akr_hip_ctx {
             d_sray[k].reserve(2 * n);
             d_scolor[k].reserve(n);
         }
-        d_L.reserve(n);
+        d_L[0].reserve(n);
+        d_L[1].reserve(n);
         d_film.reserve(n);
         cap = n;
     }
@@ -478,46 +489,56 @@ struct akr_hip_ctx {
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
         ensure_capacity(N);
         // counters per pass, each on its own 128-B line (atomics on one line serialise):
-        // M ray-queue counts, M shadow-queue counts, then 2 trace launches x kWorkWords per bounce
+        // M ray-queue counts, M shadow-queue counts, then 2 trace launches x kTraceWords per bounce;
+        // two sets, alternating by pass, since consecutive passes overlap
         const int M = p.max_depth + 2;
         const size_t n_count_words = 2 * (size_t)M * kWorkStride + 2 * (size_t)M * kTraceWords;
-        auto qcount = [&](int b) { return d_counts.p + (size_t)b * kWorkStride; };
-        auto scount = [&](int b) { return d_counts.p + (size_t)(M + b) * kWorkStride; };
-        auto work = [&](int b, int k) { return d_counts.p + 2 * (size_t)M * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
-        d_counts.reserve(n_count_words);
+        d_counts.reserve(2 * n_count_words);
         if (N == 0) return 0;
+        ensure_side_stream();
+        hipStream_t ms = main_st;
         HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
+        HIPCHK(hipEventRecord(ev_fork, st));  // both internal streams start after the caller's work
+        HIPCHK(hipStreamWaitEvent(ms, ev_fork, 0));
+        HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
         const SceneDev sd = scene_dev();
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
-        ensure_side_stream();
+        int64_t g = 0;  // bounce index over all passes: shadow queues alternate by its parity
         for (int s = 0; s < p.spp; s++) {
-            HIPCHK(hipMemsetAsync(d_counts.p, 0, n_count_words * sizeof(uint32_t), st));
-            HIPCHK(hipEventRecord(ev_fork, st));  // the side stream starts after this pass's memset
-            HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
+            const int ps = s & 1;
+            uint32_t *cnt = d_counts.p + (size_t)ps * n_count_words;
+            auto qcount = [&](int b) { return cnt + (size_t)b * kWorkStride; };
+            auto scount = [&](int b) { return cnt + (size_t)(M + b) * kWorkStride; };
+            auto work = [&](int b, int k) { return cnt + 2 * (size_t)M * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
+            float4 *L = d_L[ps].p;
+            // L[ps] and the counter set were last used by pass s - 2, whose splat ends its side-stream work
+            if (s >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ps], 0));
+            HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
             RaygenArgs rg{};
             rg.cam = cam;
             rg.pixel = d_pixel.p;
             rg.n = (uint32_t)N;
             rg.seed = d_seed.p;
-            rg.L = d_L.p;
+            rg.L = L;
             rg.ray_out = d_ray0.p;
             rg.state_out = d_state0.p;
             rg.slot_out = d_slot0.p;
             rg.count_out = qcount(0);
             rg.first_pass = s == 0;
-            timed("raygen", st, [&] { launch_raygen(rg, st); });
-            for (int b = 0; b < nb; b++) {
+            timed("raygen", ms, [&] { launch_raygen(rg, ms); });
+            for (int b = 0; b < nb; b++, g++) {
                 const bool odd = b & 1;
+                const int sq = (int)(g & 1);
                 TraceArgs t = trace_args(work(b, 0));
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
-                timed("trace_closest", st, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, st); });
-                // shade(b) refills shadow queue b % 2: the shadow trace of bounce b - 2 must be done
-                if (b >= 2) HIPCHK(hipStreamWaitEvent(st, ev_shadow[odd], 0));
+                timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
+                // shade refills shadow queue g % 2: the shadow trace of bounce g - 2 must be done
+                if (g >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_shadow[sq], 0));
                 ShadeArgs sh{};
                 sh.sc = sd;
                 sh.ray_in = odd ? d_ray1.p : d_ray0.p;
@@ -529,38 +550,43 @@ struct akr_hip_ctx {
                 sh.state_out = odd ? d_state0.p : d_state1.p;
                 sh.slot_out = odd ? d_slot0.p : d_slot1.p;
                 sh.count_out = qcount(b + 1);
-                sh.shadow_ray = d_sray[odd].p;
-                sh.shadow_color = d_scolor[odd].p;
+                sh.shadow_ray = d_sray[sq].p;
+                sh.shadow_color = d_scolor[sq].p;
                 sh.shadow_count = scount(b);
                 sh.seed = d_seed.p;
-                sh.L = d_L.p;  // written at depth 0 only, before any shadow trace of the pass
+                sh.L = L;  // written at depth 0 only, before any shadow trace of the pass
                 sh.depth = b;
                 sh.max_depth = p.max_depth;
                 sh.last = b == nb - 1;
-                timed("shade", st, [&] { launch_shade(sh, (uint32_t)N, st); });
+                timed("shade", ms, [&] { launch_shade(sh, (uint32_t)N, ms); });
+                HIPCHK(hipEventRecord(ev_shade[sq], ms));
+                HIPCHK(hipStreamWaitEvent(side, ev_shade[sq], 0));
                 if (b < p.max_depth) {
-                    HIPCHK(hipEventRecord(ev_shade[odd], st));
-                    HIPCHK(hipStreamWaitEvent(side, ev_shade[odd], 0));
                     TraceArgs ts = trace_args(work(b, 1));
                     ts.stack_ovf = d_ovf_side.p;  // concurrent with a main-stream trace
-                    ts.rays = d_sray[odd].p;
+                    ts.rays = d_sray[sq].p;
                     ts.count = scount(b);
-                    ts.shadow_color = d_scolor[odd].p;
-                    ts.L = d_L.p;
+                    ts.shadow_color = d_scolor[sq].p;
+                    ts.L = L;
                     timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, side); });
-                    HIPCHK(hipEventRecord(ev_shadow[odd], side));
                 }
+                HIPCHK(hipEventRecord(ev_shadow[sq], side));
             }
-            // splat reads L, which the shadow traces accumulate into: join the side stream
-            HIPCHK(hipEventRecord(ev_fork, side));
-            HIPCHK(hipStreamWaitEvent(st, ev_fork, 0));
+            // Tile::add_sample on the side stream, after the pass's last shadow trace: the next
+            // pass (its own L and counters) proceeds on the main stream meanwhile
             SplatArgs sp{};
-            sp.L = d_L.p;
+            sp.L = L;
             sp.film = d_film.p;
             sp.n = (uint32_t)N;
             sp.ray_clamp = p.ray_clamp;
-            timed("splat", st, [&] { launch_splat(sp, st); });
+            timed("splat", side, [&] { launch_splat(sp, side); });
+            HIPCHK(hipEventRecord(ev_splat[ps], side));
         }
+        // the caller's stream sees every pass complete
+        HIPCHK(hipEventRecord(ev_join, side));
+        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
+        HIPCHK(hipEventRecord(ev_join, ms));
+        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
         HIPCHK(hipGetLastError());
         return N;
     }
