@@ -57,7 +57,8 @@ class Rect(C.Structure):
 
 class BuildParams(C.Structure):
     _fields_ = [("max_leaf_size", C.c_int32), ("n_bins", C.c_int32), ("traversal_cost", C.c_float),
-                ("intersect_cost", C.c_float), ("n_threads", C.c_int32), ("_pad", C.c_int32 * 3)]
+                ("intersect_cost", C.c_float), ("n_threads", C.c_int32), ("builder", C.c_int32),
+                ("_pad", C.c_int32 * 2)]
 
 
 class AccelInfo(C.Structure):
@@ -78,6 +79,7 @@ class TraceCounts(C.Structure):
 
 TEX_CONSTANT, TEX_IMAGE = 0, 1
 PT_EXACT_CULL = 1
+BUILDER_SAH, BUILDER_LBVH = 0, 1
 MAT_DIFFUSE, MAT_GLOSSY, MAT_EMISSIVE, MAT_MIX = 0, 1, 2, 3
 
 # numpy views of the POD structs (for vectorised ray/hit buffers)
@@ -289,8 +291,10 @@ class HipContext:
         pw = np.ascontiguousarray(power, np.float32)
         self._check(self.lib.akr_hip_upload_lights(self.h, C.cast(arr, C.c_void_p), len(lights), _ptr(pw)))
 
-    def build_accel(self, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0, n_threads=0):
-        p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads)
+    def build_accel(self, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0, n_threads=0,
+                    builder=0):
+        """builder: BUILDER_SAH (host binned SAH) or BUILDER_LBVH (GPU Morton / Karras)."""
+        p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder)
         self._check(self.lib.akr_hip_build_accel(self.h, C.byref(p)))
         return self.accel_info()
 

@@ -30,6 +30,12 @@ struct BvhOutput {
 
 void build_bvh(const BvhInput &in, const akr_build_params &params, BvhOutput &out);
 
+#ifdef __HIPCC__
+// GPU linear BVH (lbvh.hip): Morton sort + Karras hierarchy + parallel refit on the device of the
+// current HIP context, on stream `st`; one triangle per leaf.  Same output format.
+void build_lbvh_gpu(const BvhInput &in, BvhOutput &out, hipStream_t st);
+#endif
+
 // Wide view of a BVH2 (akr_bvh4_node / akr_bvh_leaf, akr_bvh_format.h).  root_ref is the wide
 // reference of the BVH2's real root (wide node 0, a leaf, or EMPTY for an empty scene).
 struct Bvh4Output {

@@ -45,7 +45,8 @@ def measured_traffic(kernel, workload):
         except (OSError, ValueError):
             continue
         w = d.get("workload") or {}
-        if any(w.get(k) != v for k, v in workload.items()) or kernel not in d.get("kernels", {}):
+        defaults = {"builder": "sah"}  # profiles written before the key existed
+        if any(w.get(k, defaults.get(k)) != v for k, v in workload.items()) or kernel not in d.get("kernels", {}):
             continue
         best = (d["kernels"][kernel]["hbm_bytes_per_launch"], f"profiles/{p.name}")
     return best if best else (None, None)
@@ -66,6 +67,7 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--leaf", type=int, default=4)
     ap.add_argument("--sah-isect", type=float, default=4.0, help="SAH triangle-test cost (traversal step = 1)")
+    ap.add_argument("--builder", choices=["sah", "lbvh"], default="sah", help="host binned SAH or GPU LBVH")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
@@ -99,7 +101,8 @@ def main():
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
     info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect,
-                              n_threads=min(16, os.cpu_count() or 1))
+                              n_threads=min(16, os.cpu_count() or 1),
+                              builder=capi.BUILDER_LBVH if args.builder == "lbvh" else capi.BUILDER_SAH)
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)
@@ -183,7 +186,7 @@ def main():
     sh = counts["per_mode"]["shadow"]
     traffic, traffic_src = measured_traffic(TRACE_KERNEL_PROF_NAME, {
         "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf,
-        "sah_isect": args.sah_isect})
+        "sah_isect": args.sah_isect, "builder": args.builder})
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
@@ -229,7 +232,7 @@ def main():
         "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)", "triangles": cs.n_tris,
                    "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
                    "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
-                   "sah_isect": args.sah_isect},
+                   "sah_isect": args.sah_isect, "builder": args.builder},
         "roofline": roofline, "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                     for k, v in kstats.items()},

@@ -78,3 +78,35 @@ def hits_to_gid(hits, mesh_base):
     ok = hits["geom_id"] >= 0
     gid[ok] = mesh_base[hits["geom_id"][ok]] + hits["prim_id"][ok].astype(np.uint32)
     return gid
+
+
+def check_bvh(cs, nodes, tris, max_leaf):
+    """Invariants of an exported BVH2: every triangle in exactly one leaf, leaf records equal to
+    the mesh (e1, e2 as f32 subtractions), child boxes containing their subtrees, depth <= 64."""
+    n = cs.n_tris
+    assert sorted(tris["gid"].tolist()) == list(range(n)), "every triangle in exactly one leaf"
+    v = cs.vertices[cs.indices]
+    g = tris["gid"]
+    assert np.array_equal(tris["v0"], v[g, 0])
+    assert np.array_equal(tris["e1"], (v[g, 1] - v[g, 0]).astype(np.float32))
+    assert np.array_equal(tris["e2"], (v[g, 2] - v[g, 0]).astype(np.float32))
+    # walk: child boxes contain their subtree's triangles, depth bounded, leaf sizes bounded
+    stack = [(int(nodes[0]["child"][0]), nodes[0]["bxy0"], nodes[0]["bz"][:2], 1)]
+    seen = 0
+    while stack:
+        ref, bxy, bz, depth = stack.pop()
+        assert depth <= 64
+        lo = np.array([bxy[0], bxy[2], bz[0]], np.float32)
+        hi = np.array([bxy[1], bxy[3], bz[1]], np.float32)
+        if ref & 0x80000000:
+            first, cnt = (ref & 0x7FFFFFFF) >> 3, (ref & 7) + 1
+            assert cnt <= max_leaf
+            pts = v[tris["gid"][first:first + cnt]].reshape(-1, 3)
+            assert np.all(pts >= lo) and np.all(pts <= hi)
+            seen += cnt
+        else:
+            nd = nodes[ref]
+            assert nd["axis"] < 3
+            stack.append((int(nd["child"][0]), nd["bxy0"], nd["bz"][:2], depth + 1))
+            stack.append((int(nd["child"][1]), nd["bxy1"], nd["bz"][2:], depth + 1))
+    assert seen == n

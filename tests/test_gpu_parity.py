@@ -10,7 +10,7 @@ import pytest
 
 import py_oracle
 from akari_amd import capi, scene
-from helpers import cornell, edge_rays, hits_to_gid, mixed_scene, random_rays, small_soup, textured_scene
+from helpers import check_bvh, cornell, edge_rays, hits_to_gid, mixed_scene, random_rays, small_soup, textured_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -90,6 +90,37 @@ def test_trace_leaf_sizes(hip_ctx_factory, leaf):
         cs, orc = _setup(ctx, small_soup(30_000), max_leaf_size=leaf)
         assert ctx.accel_info().max_leaf <= leaf
         _check_trace(ctx, orc, cs, random_rays(1 << 14, 4, -1.1, 1.1), False)
+
+
+@pytest.mark.parametrize("n_tris", [1, 2, 37, 100_000])
+def test_gpu_lbvh_builder(hip_ctx_factory, n_tris):
+    """The GPU LBVH builder (lbvh.hip): a valid BVH2 in the same format, and
+    hits / renders bit-exact against the oracle walking that BVH with the reference algorithm."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(n_tris), builder=capi.BUILDER_LBVH)
+        nodes, tris = ctx.accel_export()
+        check_bvh(cs, nodes, tris, 1)
+        assert ctx.accel_info().max_leaf == 1
+        _check_trace(ctx, orc, cs, random_rays(1 << 14, 8, -1.2, 1.2), False)
+        _check_trace(ctx, orc, cs, random_rays(1 << 14, 9, -1.2, 1.2), True)
+        _check_trace(ctx, orc, cs, edge_rays(), False)
+        if n_tris >= 37:
+            _check_render(ctx, orc, 2, 5, [(0, 0, 96, 54)], 96, 54)
+
+
+def test_gpu_lbvh_duplicates_and_cornell(hip_ctx_factory):
+    """Identical triangles (equal Morton codes, split by index) and the Cornell box."""
+    with hip_ctx_factory(0) as ctx:
+        sc = small_soup(500)
+        m = sc.shapes[0]
+        m.vertices[3 * 100:3 * 200] = np.tile(m.vertices[0:3], (100, 1))  # triangles 100..199 = triangle 0
+        cs, orc = _setup(ctx, sc, builder=capi.BUILDER_LBVH)
+        nodes, tris = ctx.accel_export()
+        check_bvh(cs, nodes, tris, 1)
+        _check_trace(ctx, orc, cs, random_rays(1 << 12, 10, -1.2, 1.2), False)
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((32, 32)), builder=capi.BUILDER_LBVH)
+        _check_render(ctx, orc, 4, 5, [(0, 0, 32, 32)], 32, 32)
 
 
 def test_trace_empty_and_device_batch(hip_ctx_factory):

@@ -9,7 +9,7 @@ import pytest
 import py_oracle as O
 from akari_amd import capi, scene
 from conftest import CORNELL_MESH, ROOT
-from helpers import cornell, random_rays, small_soup
+from helpers import check_bvh as _check_bvh, cornell, random_rays, small_soup
 
 
 def test_library_exports_every_declared_symbol():
@@ -29,36 +29,6 @@ def test_create_without_device_fails_cleanly():
     h = C.c_void_p()
     assert capi.load_library().akr_hip_create(0, C.byref(h)) != 0 and not h.value
     assert capi.load_library().akr_hip_last_error(None) == b"null context"
-
-
-def _check_bvh(cs, nodes, tris, max_leaf):
-    n = cs.n_tris
-    assert sorted(tris["gid"].tolist()) == list(range(n)), "every triangle in exactly one leaf"
-    v = cs.vertices[cs.indices]
-    g = tris["gid"]
-    assert np.array_equal(tris["v0"], v[g, 0])
-    assert np.array_equal(tris["e1"], (v[g, 1] - v[g, 0]).astype(np.float32))
-    assert np.array_equal(tris["e2"], (v[g, 2] - v[g, 0]).astype(np.float32))
-    # walk: child boxes contain their subtree's triangles, depth bounded, leaf sizes bounded
-    stack = [(int(nodes[0]["child"][0]), nodes[0]["bxy0"], nodes[0]["bz"][:2], 1)]
-    seen = 0
-    while stack:
-        ref, bxy, bz, depth = stack.pop()
-        assert depth <= 64
-        lo = np.array([bxy[0], bxy[2], bz[0]], np.float32)
-        hi = np.array([bxy[1], bxy[3], bz[1]], np.float32)
-        if ref & 0x80000000:
-            first, cnt = (ref & 0x7FFFFFFF) >> 3, (ref & 7) + 1
-            assert cnt <= max_leaf
-            pts = v[tris["gid"][first:first + cnt]].reshape(-1, 3)
-            assert np.all(pts >= lo) and np.all(pts <= hi)
-            seen += cnt
-        else:
-            nd = nodes[ref]
-            assert nd["axis"] < 3
-            stack.append((int(nd["child"][0]), nd["bxy0"], nd["bz"][:2], depth + 1))
-            stack.append((int(nd["child"][1]), nd["bxy1"], nd["bz"][2:], depth + 1))
-    assert seen == n
 
 
 @pytest.mark.parametrize("leaf", [1, 4, 8])
