@@ -51,6 +51,10 @@ class PtParams(C.Structure):
     _fields_ = [("spp", C.c_int32), ("max_depth", C.c_int32), ("ray_clamp", C.c_float), ("flags", C.c_int32)]
 
 
+class AoParams(C.Structure):
+    _fields_ = [("spp", C.c_int32), ("occlude", C.c_float), ("flags", C.c_int32), ("_pad", C.c_int32)]
+
+
 class Rect(C.Structure):
     _fields_ = [("x0", C.c_int32), ("y0", C.c_int32), ("x1", C.c_int32), ("y1", C.c_int32)]
 
@@ -119,6 +123,7 @@ EXPORTS = {
     "akr_hip_trace": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_int]),
     "akr_hip_trace_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_int, _P]),
     "akr_hip_render": (C.c_int, [_P, C.POINTER(PtParams), _P, C.c_int32, _P, _P]),
+    "akr_hip_render_ao": (C.c_int, [_P, C.POINTER(AoParams), _P, C.c_int32, _P, _P]),
     "akr_hip_render_device": (C.c_int, [_P, C.POINTER(PtParams), _P, C.c_int32, _P, _P, _P,
                                         C.POINTER(C.c_uint64)]),
     "akr_hip_kernel_stats": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
@@ -343,6 +348,21 @@ class HipContext:
         arr, n = self._rects(tiles)
         self._check(self.lib.akr_hip_render(self.h, C.byref(p), C.cast(arr, C.c_void_p), n, _ptr(radiance),
                                             _ptr(weight)))
+        return radiance, weight
+
+    def render_ao(self, spp, tiles, width, height, occlude=float("inf"), radiance=None, weight=None,
+                  exact_cull=False):
+        """Ambient occlusion (akr_hip_render_ao), accumulated like render()."""
+        if radiance is None:
+            radiance = np.zeros((height, width, 3), np.float32)
+        if weight is None:
+            weight = np.zeros((height, width), np.float32)
+        assert radiance.dtype == np.float32 and radiance.flags.c_contiguous and radiance.size == 3 * width * height
+        assert weight.dtype == np.float32 and weight.flags.c_contiguous and weight.size == width * height
+        p = AoParams(int(spp), float(occlude), PT_EXACT_CULL if exact_cull else 0, 0)
+        arr, n = self._rects(tiles)
+        self._check(self.lib.akr_hip_render_ao(self.h, C.byref(p), C.cast(arr, C.c_void_p), n, _ptr(radiance),
+                                               _ptr(weight)))
         return radiance, weight
 
     def render_device(self, spp, max_depth, tiles, d_radiance: int, d_weight: int, stream: int = 0, ray_clamp=0.0):

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <algorithm>
 #include <string>
+#include <limits>
 #include <vector>
 
 #include "../../include/akr_hip.h"
@@ -250,6 +251,28 @@ class HipPathTracer {
               akr_hip_render_node(h.data(), (int32_t)h.size(), &p, tiles.data(), (int32_t)tiles.size(),
                                   film.radiance.data(), film.weight.data()),
               "render_node");
+    }
+};
+
+// cpu::AmbientOcclusion<C> (spp, occlude; kernel/integrators/cpu/integrator.h:35-45), rendered on
+// the GPU through akr_hip_render_ao.
+class HipAmbientOcclusion {
+  public:
+    int spp = 16, tile_size = 16;
+    float occlude = std::numeric_limits<float>::infinity();
+    HipAmbientOcclusion() = default;
+    HipAmbientOcclusion(int spp_, float occlude_) : spp(spp_), occlude(occlude_) {}
+
+    void render(const HipAccelerator &scene, Film &film) const {
+        const int ts = std::max(16, tile_size);  // one call renders every tile: size is a batching knob
+        std::vector<akr_rect> tiles;
+        for (int y = 0; y < film.height; y += ts)
+            for (int x = 0; x < film.width; x += ts) tiles.push_back({x, y, x + ts, y + ts});
+        akr_ao_params p{spp, occlude, 0, 0};
+        check(scene.handle(),
+              akr_hip_render_ao(scene.handle(), &p, tiles.data(), (int32_t)tiles.size(), film.radiance.data(),
+                                film.weight.data()),
+              "render_ao");
     }
 };
 

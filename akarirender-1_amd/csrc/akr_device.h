@@ -131,6 +131,30 @@ struct ShadeArgs {
     int32_t last;                  // no extension ray is traced after this bounce
 };
 
+// One AO bounce (cpu/integrator.cpp:46-56) for every queued camera hit: appends the AO ray to
+// ray_out (+ colour (1,1,1, slot) for a shadow-mode trace, or the slot for a closest-hit trace).
+struct AoShadeArgs {
+    const ShadeTri *tri;
+    const float4 *hit_in;
+    const uint32_t *slot_in;
+    const float4 *state_in;        // seed bits in .w
+    const uint32_t *count_in;
+    uint32_t *seed;                // per slot: the sampler state after the sample
+    float4 *ray_out;
+    float4 *color_out;             // shadow-mode queue: (1, 1, 1, slot bits), or nullptr
+    uint32_t *slot_out;            // closest-hit queue: slot, or nullptr
+    uint32_t *count_out;
+};
+
+// After a closest-hit AO trace: L[slot] += 1 unless the hit has t < occlude.
+struct AoResolveArgs {
+    const float4 *hits;            // (t, u, v, gid bits) per queue entry
+    const uint32_t *slot;
+    const uint32_t *count;
+    float4 *L;
+    float occlude;
+};
+
 struct RaygenArgs {
     CameraDev cam;
     const uint32_t *pixel;         // per slot: x | y << 16

@@ -182,6 +182,7 @@ struct akr_hip_ctx {
     DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_film;
     DBuf<float4> d_L[2];  // per-sample radiance, alternating by sample pass (passes overlap)
     DBuf<float4> d_sray[2], d_scolor[2];  // shadow queues, alternating by bounce
+    DBuf<uint32_t> d_ao_slot[2];          // AO queues traced closest-hit (finite occlude): slots
     // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
     // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
     // Both internal: `main` (high priority) runs raygen / closest-hit / shade, `side` (low priority)
@@ -472,11 +473,11 @@ struct akr_hip_ctx {
         HIPCHK(hipGetLastError());
     }
 
-    uint64_t render(const akr_pt_params &p, const akr_rect *tiles, int32_t n_tiles, hipStream_t st) {
+    // Pixels of the tile list (tiles in order, row-major inside a tile) into h_pixel / d_pixel;
+    // sizes the queues and the per-pass counter sets.  Returns the pixel count.
+    uint64_t setup_pixels(const akr_rect *tiles, int32_t n_tiles, size_t n_count_words, hipStream_t st) {
         require_ready();
         if (!cam_set) throw std::runtime_error("camera not set (call akr_hip_set_camera)");
-        if (p.spp < 0 || p.max_depth < 0) throw std::runtime_error("spp and max_depth must be >= 0");
-        if (p.max_depth > 1000) throw std::runtime_error("max_depth too large");
         if (n_tiles < 0 || (n_tiles > 0 && !tiles)) throw std::runtime_error("invalid tile list");
         h_pixel.clear();
         for (int k = 0; k < n_tiles; k++) {
@@ -488,20 +489,52 @@ struct akr_hip_ctx {
         const uint64_t N = h_pixel.size();
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
         ensure_capacity(N);
+        d_counts.reserve(2 * n_count_words);
+        if (N == 0) return 0;
+        ensure_side_stream();
+        HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
+        HIPCHK(hipEventRecord(ev_fork, st));  // both internal streams start after the caller's work
+        HIPCHK(hipStreamWaitEvent(main_st, ev_fork, 0));
+        HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
+        return N;
+    }
+
+    // the caller's stream sees every pass of both internal streams complete
+    void join_streams(hipStream_t st) {
+        HIPCHK(hipEventRecord(ev_join, side));
+        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
+        HIPCHK(hipEventRecord(ev_join, main_st));
+        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
+        HIPCHK(hipGetLastError());
+    }
+
+    RaygenArgs raygen_args(uint32_t N, float4 *L, uint32_t *count, bool first) const {
+        RaygenArgs rg{};
+        rg.cam = cam;
+        rg.pixel = d_pixel.p;
+        rg.n = N;
+        rg.seed = d_seed.p;
+        rg.L = L;
+        rg.ray_out = d_ray0.p;
+        rg.state_out = d_state0.p;
+        rg.slot_out = d_slot0.p;
+        rg.count_out = count;
+        rg.first_pass = first;
+        return rg;
+    }
+
+    uint64_t render(const akr_pt_params &p, const akr_rect *tiles, int32_t n_tiles, hipStream_t st) {
+        if (p.spp < 0 || p.max_depth < 0) throw std::runtime_error("spp and max_depth must be >= 0");
+        if (p.max_depth > 1000) throw std::runtime_error("max_depth too large");
         // counters per pass, each on its own 128-B line (atomics on one line serialise):
         // M ray-queue counts, M shadow-queue counts, then 2 trace launches x kTraceWords per bounce;
         // two sets, alternating by pass, since consecutive passes overlap
         const int M = p.max_depth + 2;
         const size_t n_count_words = 2 * (size_t)M * kWorkStride + 2 * (size_t)M * kTraceWords;
-        d_counts.reserve(2 * n_count_words);
+        const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st);
         if (N == 0) return 0;
-        ensure_side_stream();
         hipStream_t ms = main_st;
-        HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
-        HIPCHK(hipEventRecord(ev_fork, st));  // both internal streams start after the caller's work
-        HIPCHK(hipStreamWaitEvent(ms, ev_fork, 0));
-        HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
         const SceneDev sd = scene_dev();
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
@@ -517,17 +550,7 @@ struct akr_hip_ctx {
             // L[ps] and the counter set were last used by pass s - 2, whose splat ends its side-stream work
             if (s >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ps], 0));
             HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
-            RaygenArgs rg{};
-            rg.cam = cam;
-            rg.pixel = d_pixel.p;
-            rg.n = (uint32_t)N;
-            rg.seed = d_seed.p;
-            rg.L = L;
-            rg.ray_out = d_ray0.p;
-            rg.state_out = d_state0.p;
-            rg.slot_out = d_slot0.p;
-            rg.count_out = qcount(0);
-            rg.first_pass = s == 0;
+            const RaygenArgs rg = raygen_args((uint32_t)N, L, qcount(0), s == 0);
             timed("raygen", ms, [&] { launch_raygen(rg, ms); });
             for (int b = 0; b < nb; b++, g++) {
                 const bool odd = b & 1;
@@ -582,12 +605,81 @@ struct akr_hip_ctx {
             timed("splat", side, [&] { launch_splat(sp, side); });
             HIPCHK(hipEventRecord(ev_splat[ps], side));
         }
-        // the caller's stream sees every pass complete
-        HIPCHK(hipEventRecord(ev_join, side));
-        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
-        HIPCHK(hipEventRecord(ev_join, ms));
-        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
-        HIPCHK(hipGetLastError());
+        join_streams(st);
+        return N;
+    }
+
+    // cpu::AmbientOcclusion::render (kernel/integrators/cpu/integrator.cpp:40-87) as one wavefront
+    // pass per sample: raygen -> closest-hit trace -> k_ao_shade on the main stream, then the AO
+    // rays and splat on the side stream (overlapping the next pass, as in render()).  occlude = +inf
+    // makes "closest hit with t < occlude" plain occlusion (any hit in (Eps, inf)): a shadow-mode
+    // trace adds 1 to L when unoccluded.  Any other occlude traces the AO rays closest-hit and
+    // compares t (an any-hit trace bounded by tmax = occlude could differ from the reference by
+    // float rounding in the box tests near t = occlude).
+    uint64_t render_ao(const akr_ao_params &p, const akr_rect *tiles, int32_t n_tiles, hipStream_t st) {
+        if (p.spp < 0) throw std::runtime_error("spp must be >= 0");
+        // per pass: camera-queue count, AO-queue count, then 2 trace launches x kTraceWords
+        const size_t n_count_words = 2 * (size_t)kWorkStride + 2 * (size_t)kTraceWords;
+        const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st);
+        if (N == 0) return 0;
+        const bool shadow_mode = std::isinf(p.occlude) && p.occlude > 0;
+        if (!shadow_mode)
+            for (int k = 0; k < 2; k++) d_ao_slot[k].reserve(N);
+        hipStream_t ms = main_st;
+        const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
+        for (int s = 0; s < p.spp; s++) {
+            const int ps = s & 1;
+            uint32_t *cnt = d_counts.p + (size_t)ps * n_count_words;
+            uint32_t *qcount = cnt, *acount = cnt + kWorkStride;
+            uint32_t *work0 = cnt + 2 * kWorkStride, *work1 = work0 + kTraceWords;
+            float4 *L = d_L[ps].p;
+            // L[ps], the AO queue ps and the counter set were last used by pass s - 2 (ends with its splat)
+            if (s >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ps], 0));
+            HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
+            const RaygenArgs rg = raygen_args((uint32_t)N, L, qcount, s == 0);
+            timed("raygen", ms, [&] { launch_raygen(rg, ms); });
+            TraceArgs t = trace_args(work0);
+            t.rays = d_ray0.p;
+            t.count = qcount;
+            t.hits = d_hit.p;
+            timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
+            AoShadeArgs sh{};
+            sh.tri = d_shade_tri.p;
+            sh.hit_in = d_hit.p;
+            sh.slot_in = d_slot0.p;
+            sh.state_in = d_state0.p;
+            sh.count_in = qcount;
+            sh.seed = d_seed.p;
+            sh.ray_out = d_sray[ps].p;
+            sh.color_out = shadow_mode ? d_scolor[ps].p : nullptr;
+            sh.slot_out = shadow_mode ? nullptr : d_ao_slot[ps].p;
+            sh.count_out = acount;
+            timed("ao_shade", ms, [&] { launch_ao_shade(sh, (uint32_t)N, ms); });
+            HIPCHK(hipEventRecord(ev_shade[ps], ms));
+            HIPCHK(hipStreamWaitEvent(side, ev_shade[ps], 0));
+            TraceArgs ts = trace_args(work1);
+            ts.stack_ovf = d_ovf_side.p;  // concurrent with the next pass's main-stream trace
+            ts.rays = d_sray[ps].p;
+            ts.count = acount;
+            if (shadow_mode) {
+                ts.shadow_color = d_scolor[ps].p;
+                ts.L = L;
+                timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, side); });
+            } else {
+                ts.hits = d_scolor[ps].p;  // the colour queue is free in this mode: AO hits
+                timed("trace_ao_closest", side, [&] { trace_launch(TRACE_CLOSEST, tight, ts, N, side); });
+                AoResolveArgs rs{d_scolor[ps].p, d_ao_slot[ps].p, acount, L, p.occlude};
+                timed("ao_resolve", side, [&] { launch_ao_resolve(rs, (uint32_t)N, side); });
+            }
+            SplatArgs sp{};
+            sp.L = L;
+            sp.film = d_film.p;
+            sp.n = (uint32_t)N;
+            sp.ray_clamp = 0.0f;  // Tile::add_sample(p, L, 1) unclamped (integrator.cpp:78)
+            timed("splat", side, [&] { launch_splat(sp, side); });
+            HIPCHK(hipEventRecord(ev_splat[ps], side));
+        }
+        join_streams(st);
         return N;
     }
 };
@@ -900,25 +992,39 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
     return 0;
 }
 
+namespace {
+// Film::merge_tile (core/film.h:85-95) of the context's packed film into full-frame host buffers
+void merge_film(akr_hip_ctx *ctx, uint64_t N, float *radiance, float *weight) {
+    if (N == 0) return;
+    hipStream_t st = ctx->stream;
+    std::vector<float4> film(N);
+    HIPCHK(hipMemcpyAsync(film.data(), ctx->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int W = ctx->cam.width;
+    for (uint64_t k = 0; k < N; k++) {
+        uint32_t px = ctx->h_pixel[k];
+        uint64_t pix = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
+        radiance[3 * pix + 0] += film[k].x;
+        radiance[3 * pix + 1] += film[k].y;
+        radiance[3 * pix + 2] += film[k].z;
+        weight[pix] += film[k].w;
+    }
+}
+}  // namespace
+
 int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles, int32_t n_tiles,
                    float *radiance, float *weight) {
     return guard(ctx, [&] {
         if (!params || !radiance || !weight) throw std::runtime_error("null argument");
-        hipStream_t st = ctx->stream;
-        uint64_t N = ctx->render(*params, tiles, n_tiles, st);
-        if (N == 0) return;
-        std::vector<float4> film(N);
-        HIPCHK(hipMemcpyAsync(film.data(), ctx->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        const int W = ctx->cam.width;
-        for (uint64_t k = 0; k < N; k++) {  // Film::merge_tile (core/film.h:85-95)
-            uint32_t px = ctx->h_pixel[k];
-            uint64_t pix = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
-            radiance[3 * pix + 0] += film[k].x;
-            radiance[3 * pix + 1] += film[k].y;
-            radiance[3 * pix + 2] += film[k].z;
-            weight[pix] += film[k].w;
-        }
+        merge_film(ctx, ctx->render(*params, tiles, n_tiles, ctx->stream), radiance, weight);
+    });
+}
+
+int akr_hip_render_ao(akr_hip_ctx *ctx, const akr_ao_params *params, const akr_rect *tiles, int32_t n_tiles,
+                      float *radiance, float *weight) {
+    return guard(ctx, [&] {
+        if (!params || !radiance || !weight) throw std::runtime_error("null argument");
+        merge_film(ctx, ctx->render_ao(*params, tiles, n_tiles, ctx->stream), radiance, weight);
     });
 }
 

@@ -12,6 +12,8 @@ int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_splat(const SplatArgs &a, hipStream_t st);
+void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st);
+void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t st);
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st);
 
 }  // namespace akr

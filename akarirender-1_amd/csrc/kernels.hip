@@ -808,6 +808,58 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
     }
 }
 
+// --------------------------------------------------------------------------- ambient occlusion
+// cpu::AmbientOcclusion's Li after the camera ray (kernel/integrators/cpu/integrator.cpp:46-56):
+// on a hit, one cosine-hemisphere direction in the frame of the geometric normal, from trig.p(uv)
+// with the default tmin Eps; the sampler state is persisted for the next sample pass either way.
+__global__ __launch_bounds__(kBlock) void k_ao_shade(AoShadeArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = *a.count_in;
+    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup: before the barrier
+    bool want = false;
+    float4 r0 = {}, r1 = {};
+    uint32_t slot = 0;
+    if (i < n) {
+        slot = a.slot_in[i];
+        uint32_t seed = fbits(a.state_in[i].w);
+        const float4 hv = a.hit_in[i];
+        const uint32_t gid = fbits(hv.w);
+        if (gid != kNoHit) {
+            const ShadeTri tr = a.tri[gid];
+            const V3 v0{tr.a.x, tr.a.y, tr.a.z}, v1{tr.b.x, tr.b.y, tr.b.z}, v2{tr.c.x, tr.c.y, tr.c.z};
+            const Frame frame = make_frame(normalize(cross(sub(v1, v0), sub(v2, v0))));
+            const V3 w = to_world(frame, cosine_hemisphere(lcg_next2(seed)));
+            const V3 p = lerp3(v0, v1, v2, hv.y, hv.z);
+            want = true;
+            r0 = make_float4(p.x, p.y, p.z, kEps);
+            r1 = make_float4(w.x, w.y, w.z, kInf);
+        }
+        a.seed[slot] = seed;
+    }
+    uint32_t pos, unused;
+    block_append2(want, a.count_out, pos, false, a.count_out, unused);
+    if (want) {
+        a.ray_out[2 * (size_t)pos] = r0;
+        a.ray_out[2 * (size_t)pos + 1] = r1;
+        if (a.color_out) a.color_out[pos] = make_float4(1.0f, 1.0f, 1.0f, bitsf(slot));
+        if (a.slot_out) a.slot_out[pos] = slot;
+    }
+}
+
+// `scene.intersect(ray, &its) && its.t < occlude` -> 0, else 1 (integrator.cpp:53-55)
+__global__ __launch_bounds__(kBlock) void k_ao_resolve(AoResolveArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *a.count) return;
+    const float4 h = a.hits[i];
+    if (fbits(h.w) != kNoHit && h.x < a.occlude) return;
+    const uint32_t slot = a.slot[i];
+    float4 l = a.L[slot];
+    l.x += 1.0f;
+    l.y += 1.0f;
+    l.z += 1.0f;
+    a.L[slot] = l;
+}
+
 // ------------------------------------------------------------------------------------- splat
 __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -887,6 +939,14 @@ void launch_raygen(const RaygenArgs &a, hipStream_t st) {
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_shade, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+}
+void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items == 0) return;
+    hipLaunchKernelGGL(k_ao_shade, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+}
+void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items == 0) return;
+    hipLaunchKernelGGL(k_ao_resolve, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
 void launch_splat(const SplatArgs &a, hipStream_t st) {
     if (a.n == 0) return;

@@ -108,6 +108,15 @@ typedef struct akr_pt_params {
     int32_t flags;
 } akr_pt_params;
 
+/* Ambient-occlusion integrator parameters (cpu::AmbientOcclusion, kernel/integrators/cpu/
+ * integrator.h:35-45; AOIntegratorNode defaults spp 16, occlude +inf, core/nodes/integrator.cpp:26-49). */
+typedef struct akr_ao_params {
+    int32_t spp;
+    float occlude;  /* a closest hit of the AO ray with t < occlude occludes it */
+    int32_t flags;  /* AKR_PT_EXACT_CULL */
+    int32_t _pad;
+} akr_ao_params;
+
 /* Pixel rectangle [x0, x1) x [y0, y1). */
 typedef struct akr_rect {
     int32_t x0, y0, x1, y1;
@@ -194,6 +203,14 @@ int akr_hip_trace_device(akr_hip_ctx *ctx, const void *d_rays, uint64_t n, void 
  * Film's Pixel{radiance, weight} (core/film.h:31-35).  Synchronous. */
 int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles,
                    int32_t n_tiles, float *radiance, float *weight);
+/* cpu::AmbientOcclusion::render (kernel/integrators/cpu/integrator.cpp:40-87) — replaces
+ * AOIntegrator::render (core/nodes/integrator.cpp:33-38) for the pixels of `tiles`: per sample,
+ * L = 1 if the camera ray hits and the cosine-sampled ray about the geometric normal from the hit
+ * point has no closest hit with t < occlude, else 0; accumulated like akr_hip_render.  Reuses the
+ * path tracer's raygen / closest-hit trace; with occlude = +inf the AO ray is an occlusion query
+ * (shadow-mode trace), otherwise a closest-hit trace whose t is compared.  Synchronous. */
+int akr_hip_render_ao(akr_hip_ctx *ctx, const akr_ao_params *params, const akr_rect *tiles,
+                      int32_t n_tiles, float *radiance, float *weight);
 /* Multi-GPU render from one host process (SURVEY.md §8b akr_hip_render_node): tile j goes to
  * ctxs[j % n_ctx] (one context per device, each holding the same scene and camera), the contexts
  * render concurrently on one host thread each, and their films are merged into the host buffers

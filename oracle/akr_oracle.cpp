@@ -652,6 +652,43 @@ void parallel_for(uint64_t n, int threads, uint64_t chunk, F &&f) {
     for (auto &t : ts) t.join();
 }
 
+// split every rect into 16x16 work tiles (cpu/integrator.h:47, TileSize film.h:37)
+struct Work { int x0, y0, x1, y1; };
+std::vector<Work> split_work(const akr_rect *tiles, int n_tiles, int W, int H) {
+    std::vector<Work> work;
+    for (int k = 0; k < n_tiles; k++) {
+        int x0 = std::max(0, tiles[k].x0), y0 = std::max(0, tiles[k].y0);
+        int x1 = std::min(W, tiles[k].x1), y1 = std::min(H, tiles[k].y1);
+        for (int ty = y0; ty < y1; ty += 16)
+            for (int tx = x0; tx < x1; tx += 16) work.push_back({tx, ty, std::min(x1, tx + 16), std::min(y1, ty + 16)});
+    }
+    return work;
+}
+
+// cpu::AmbientOcclusion::render's Li (kernel/integrators/cpu/integrator.cpp:43-60).  The camera
+// sample is generate_ray(sampler.next2d(), sampler.next2d(), p) (:76-77): C++ leaves the order of
+// the two argument evaluations unspecified; we take them left to right (lens draw first, film draw
+// second), the order the path tracer's camera_ray spells out (pathtracer.h:61-64), so the AO and
+// path-traced camera rays of a sample coincide.
+float trace_ao(const Scene &sc, Lcg &sampler, int x, int y, float occlude, bool tight, PathStats &st) {
+    const orc_scene &s = *sc.s;
+    V2 u1 = sampler.next2d();  // lens sample (unused: lens_radius = 0)
+    (void)u1;
+    V2 u2 = sampler.next2d();
+    Ray ray = to_ray(generate_ray(sc.cam, u2, x, y));
+    st.cam++;
+    Best hit;
+    if (!traverse(s, ray, false, tight, hit, st.box, st.tri)) return 0.0f;
+    Tri tri = get_triangle(s, hit.gid);
+    Frame frame = make_frame(tri_ng(tri));  // Frame3f frame(trig.ng())
+    V3 w = to_world(frame, cosine_hemisphere(sampler.next2d()));
+    Ray ao{lerp3(tri.v[0], tri.v[1], tri.v[2], hit.u, hit.v), w, kEps, kInf};  // Ray3f(trig.p(uv), w)
+    st.shd++;
+    Best h2;
+    if (traverse(s, ao, false, tight, h2, st.box, st.tri) && h2.t < occlude) return 0.0f;
+    return 1.0f;
+}
+
 }  // namespace
 
 extern "C" {
@@ -754,15 +791,7 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
         for (int i = 0; i < s->n_lights; i++) sc.lights.push_back(get_triangle(*s, s->light_gid[i]));
     }
     const int W = sc.cam.w, H = sc.cam.h;
-    // split every rect into 16x16 work tiles (cpu/integrator.h:47, TileSize film.h:37)
-    struct Work { int x0, y0, x1, y1; };
-    std::vector<Work> work;
-    for (int k = 0; k < n_tiles; k++) {
-        int x0 = std::max(0, tiles[k].x0), y0 = std::max(0, tiles[k].y0);
-        int x1 = std::min(W, tiles[k].x1), y1 = std::min(H, tiles[k].y1);
-        for (int ty = y0; ty < y1; ty += 16)
-            for (int tx = x0; tx < x1; tx += 16) work.push_back({tx, ty, std::min(x1, tx + 16), std::min(y1, ty + 16)});
-    }
+    const std::vector<Work> work = split_work(tiles, n_tiles, W, H);
     int T = hw_threads(n_threads);
     std::vector<PathStats> pst(T);
     const float clampv = p->ray_clamp;
@@ -798,6 +827,45 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
         for (auto &q : pst) {
             stats->camera_rays += q.cam;
             stats->extension_rays += q.ext;
+            stats->shadow_rays += q.shd;
+            stats->box_tests += q.box;
+            stats->tri_tests += q.tri;
+        }
+    }
+    return 0;
+}
+
+int orc_render_ao(const orc_scene *s, const akr_ao_params *p, const akr_rect *tiles, int32_t n_tiles, float *radiance,
+                  float *weight, int32_t n_threads, orc_render_stats *stats) {
+    Scene sc;
+    sc.s = s;
+    sc.cam = make_camera(s->camera);
+    const int W = sc.cam.w, H = sc.cam.h;
+    const std::vector<Work> work = split_work(tiles, n_tiles, W, H);
+    int T = hw_threads(n_threads);
+    std::vector<PathStats> pst(T);
+    const bool tight = !(p->flags & AKR_PT_EXACT_CULL);
+    parallel_for(work.size(), T, 1, [&](uint64_t wi, int tid) {
+        const Work &w = work[wi];
+        for (int y = w.y0; y < w.y1; y++)
+            for (int x = w.x0; x < w.x1; x++) {
+                Lcg sampler{(uint32_t)(x + y * W)};  // set_sample_index(x + y * W), integrator.cpp:73
+                float acc = 0, wsum = 0;
+                for (int sidx = 0; sidx < p->spp; sidx++) {
+                    acc += trace_ao(sc, sampler, x, y, p->occlude, tight, pst[tid]);  // Spectrum(L) per channel
+                    wsum += 1.0f;
+                }
+                int64_t pix = (int64_t)x + (int64_t)y * W;
+                radiance[3 * pix + 0] += acc;  // Film::merge_tile, film.h:85-95
+                radiance[3 * pix + 1] += acc;
+                radiance[3 * pix + 2] += acc;
+                weight[pix] += wsum;
+            }
+    });
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        for (auto &q : pst) {
+            stats->camera_rays += q.cam;
             stats->shadow_rays += q.shd;
             stats->box_tests += q.box;
             stats->tri_tests += q.tri;

@@ -94,6 +94,12 @@ int orc_trace_brute(const orc_scene *s, const akr_ray *rays, uint64_t n, orc_hit
  * (core/parallel.cpp:44-129); accumulates into full-frame radiance[W*H*3], weight[W*H]. */
 int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles, int32_t n_tiles,
                float *radiance, float *weight, int32_t n_threads, orc_render_stats *stats);
+/* cpu::AmbientOcclusion::render (kernel/integrators/cpu/integrator.cpp:40-87) over the pixels of
+ * `tiles`, same work split; L is 1 when the cosine-sampled ray from the camera hit (frame of the
+ * geometric normal, tmin Eps) has no closest hit with t < occlude, 0 otherwise or on a camera miss.
+ * AO rays are counted as stats->shadow_rays. */
+int orc_render_ao(const orc_scene *s, const akr_ao_params *p, const akr_rect *tiles, int32_t n_tiles,
+                  float *radiance, float *weight, int32_t n_threads, orc_render_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -66,6 +66,7 @@ def lib():
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.orc_trace_brute.argtypes = [C.POINTER(OrcScene), _P, C.c_uint64, _P, C.c_int, C.c_int32]
         l.orc_render.argtypes = [C.POINTER(OrcScene), _P, _P, C.c_int32, _P, _P, C.c_int32, C.POINTER(OrcStats)]
+        l.orc_render_ao.argtypes = [C.POINTER(OrcScene), _P, _P, C.c_int32, _P, _P, C.c_int32, C.POINTER(OrcStats)]
         _lib = l
     return _lib
 
@@ -210,4 +211,23 @@ class OracleScene:
                          n_threads, C.byref(st))
         stats = dict(camera_rays=st.camera_rays, extension_rays=st.extension_rays, shadow_rays=st.shadow_rays,
                      box_tests=st.box_tests, tri_tests=st.tri_tests)
+        return radiance, weight, stats
+
+    def render_ao(self, spp, tiles=None, occlude=float("inf"), n_threads=0, radiance=None, weight=None,
+                  exact_cull=False):
+        """cpu::AmbientOcclusion::render restated (orc_render_ao); AO rays count as shadow_rays."""
+        W, H = self.width, self.height
+        if tiles is None:
+            tiles = [(0, 0, W, H)]
+        if radiance is None:
+            radiance = np.zeros((H, W, 3), np.float32)
+        if weight is None:
+            weight = np.zeros((H, W), np.float32)
+        p = self.capi.AoParams(int(spp), float(occlude), 1 if exact_cull else 0, 0)
+        rects = (self.capi.Rect * max(1, len(tiles)))(*[self.capi.Rect(*t) for t in tiles])
+        st = OrcStats()
+        lib().orc_render_ao(C.byref(self.s), C.byref(p), C.cast(rects, _P), len(tiles), _p(radiance), _p(weight),
+                            n_threads, C.byref(st))
+        stats = dict(camera_rays=st.camera_rays, shadow_rays=st.shadow_rays, box_tests=st.box_tests,
+                     tri_tests=st.tri_tests)
         return radiance, weight, stats

@@ -1,6 +1,7 @@
 // adapter_demo.cpp — renders the reference's Cornell fixture through the C++ host adapter
 // (akari_hip.hpp: HipAccelerator + HipPathTracer + Film), the way a reference-side integration
-// would call it.  Usage: adapter_demo <CornellBox-Original.obj.mesh> <out.pfm> <w> <h> <spp>
+// would call it.  Usage: adapter_demo <CornellBox-Original.obj.mesh> <out.pfm> <w> <h> <spp> [ao]
+// ("ao": HipAmbientOcclusion instead of HipPathTracer)
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -71,8 +72,13 @@ int main(int argc, char **argv) {
     bool hit = accel.intersect(r, &h);
     bool occ = accel.occlude(r);
     Film film(s.camera.resolution[0], s.camera.resolution[1]);
-    HipPathTracer pt(std::atoi(argv[5]), 5, 16, 0.0f);
-    pt.render(accel, film);
+    if (argc > 6 && std::strcmp(argv[6], "ao") == 0) {
+        HipAmbientOcclusion ao(std::atoi(argv[5]), std::numeric_limits<float>::infinity());
+        ao.render(accel, film);
+    } else {
+        HipPathTracer pt(std::atoi(argv[5]), 5, 16, 0.0f);
+        pt.render(accel, film);
+    }
     double sum = 0;
     for (float x : film.radiance) sum += x;
     film.write_pfm(argv[2]);

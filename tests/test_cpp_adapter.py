@@ -39,3 +39,20 @@ def test_adapter_render_matches_python_binding(tmp_path):
         scene.upload_scene(ctx, cs)
         rad, w = ctx.render(4, 5, [(0, 0, 32, 32)], 32, 32)
     assert np.array_equal(pfm, rad / w[..., None])
+
+
+@pytest.mark.gpu
+def test_adapter_ao_matches_python_binding(tmp_path):
+    exe = _build(tmp_path)
+    out = tmp_path / "cornell_ao.pfm"
+    r = subprocess.run([str(exe), str(CORNELL_MESH), str(out), "32", "32", "4", "ao"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    raw = out.read_bytes()
+    header_end = raw.index(b"-1.0\n") + 5
+    pfm = np.frombuffer(raw[header_end:], np.float32).reshape(32, 32, 3)[::-1]
+    cs = scene.compile_scene(scene.cornell_scene(CORNELL_MESH, resolution=(32, 32)))
+    with capi.HipContext(0) as ctx:
+        scene.upload_scene(ctx, cs)
+        rad, w = ctx.render_ao(4, [(0, 0, 32, 32)], 32, 32)
+    assert np.array_equal(pfm, rad / w[..., None])

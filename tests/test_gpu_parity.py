@@ -243,3 +243,49 @@ def test_render_device_packed(hip_ctx_factory):
             blk = orad[y0:y1, x0:x1].reshape(-1, 3)
             assert np.array_equal(r[k:k + blk.shape[0]], blk)
             k += blk.shape[0]
+
+
+def _check_ao(ctx, orc, spp, tiles, W, H, occlude=float("inf"), exact=False):
+    rad, w = ctx.render_ao(spp, tiles, W, H, occlude=occlude, exact_cull=exact)
+    orad, ow, _ = orc.render_ao(spp, tiles=tiles, occlude=occlude, exact_cull=exact)
+    assert np.array_equal(w, ow)
+    bad = rad != orad
+    assert not bad.any(), f"{bad.sum()} AO values differ (occlude={occlude})"
+    return rad, w
+
+
+@pytest.mark.parametrize("occlude", [float("inf"), 0.5])
+def test_render_ao_cornell_bit_exact(hip_ctx_factory, occlude):
+    """cpu::AmbientOcclusion (integrator.cpp:40-87): +inf runs the AO rays as a shadow-mode
+    occlusion trace, a finite distance as a closest-hit trace compared against occlude."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((48, 40)))
+        rad, w = _check_ao(ctx, orc, 16, [(0, 0, 48, 40)], 48, 40, occlude=occlude)
+        assert np.all(w == 16) and 0 < rad.mean() < 16
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_render_ao_soup_bit_exact(hip_ctx_factory, exact):
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(50_000, (64, 36)))
+        for occlude in (float("inf"), 0.05):
+            _check_ao(ctx, orc, 4, [(0, 0, 64, 36)], 64, 36, occlude=occlude, exact=exact)
+
+
+def test_render_ao_edges(hip_ctx_factory):
+    """Ragged / clipped / empty tiles, spp 0, an empty tile list, and the degenerate occlude
+    values (0, negative, NaN: t < occlude never holds, every camera hit scores 1)."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((40, 24)))
+        tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]
+        for occlude in (float("inf"), 1e30, 1.0, 0.0, -1.0, float("nan")):
+            _check_ao(ctx, orc, 3, tiles, 40, 24, occlude=occlude)
+        a, _ = ctx.render_ao(3, tiles, 40, 24)
+        b, _ = ctx.render_ao(3, tiles, 40, 24, occlude=1e30)   # closest-hit path, same answer
+        assert np.array_equal(a, b)
+        rad, w = ctx.render_ao(0, tiles, 40, 24)
+        assert not w.any() and not rad.any()
+        rad, w = ctx.render_ao(2, [], 40, 24)
+        assert not w.any()
+        # the path tracer after AO on the same context still matches its oracle
+        _check_render(ctx, orc, 2, 5, tiles, 40, 24)

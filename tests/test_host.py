@@ -171,6 +171,42 @@ def test_oracle_render_tiles_accumulate_and_threads():
     assert np.array_equal(r2, 2 * full) and np.all(w2 == 6)
 
 
+def test_oracle_ao_properties():
+    """cpu::AmbientOcclusion restated (integrator.cpp:40-87): L per sample is 0 or 1 on all three
+    channels, monotone in `occlude` for the same sample streams, 1 for every camera hit when
+    occlude <= 0 (t < occlude never holds), and 0 on a camera miss."""
+    cs = scene.compile_scene(cornell((24, 16)))
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    orc = O.OracleScene(cs, nodes, tris, capi)
+    spp = 6
+    inf, wi, st = orc.render_ao(spp)
+    assert np.all(wi == spp)
+    assert np.array_equal(inf[..., 0], inf[..., 1]) and np.array_equal(inf[..., 0], inf[..., 2])
+    assert np.array_equal(inf, np.round(inf)) and inf.min() >= 0 and inf.max() <= spp
+    near, _, _ = orc.render_ao(spp, occlude=0.25)
+    far, _, _ = orc.render_ao(spp, occlude=2.0)
+    hitmask, _, s0 = orc.render_ao(spp, occlude=0.0)
+    assert np.all(inf <= far) and np.all(far <= near) and np.all(near <= hitmask)
+    assert (near > inf).any() and inf.mean() > 0
+    assert s0["camera_rays"] == 24 * 16 * spp and s0["shadow_rays"] == hitmask[..., 0].sum()
+    assert st["shadow_rays"] == s0["shadow_rays"]
+    # exact culling is a traversal detail: same image
+    ex, _, _ = orc.render_ao(spp, exact_cull=True)
+    assert np.array_equal(ex, inf)
+    # a lone quad: nothing can occlude its AO rays, whichever side they leave from
+    quad = scene.Mesh(vertices=np.array([[-5, -5, 0], [5, -5, 0], [5, 5, 0], [-5, 5, 0]], np.float32),
+                      indices=np.array([[0, 1, 2], [0, 2, 3]], np.int32),
+                      normals=np.tile(np.array([0, 0, 1], np.float32), (2, 3)),
+                      texcoords=np.zeros((2, 6), np.float32), material_indices=np.zeros(2, np.int32),
+                      materials=[scene.DiffuseMaterial(scene.ConstantTexture((0.5, 0.5, 0.5)))])
+    qs = scene.compile_scene(scene.Scene(camera=scene.PerspectiveCamera(position=(0, 0, 4), resolution=(12, 8),
+                                                                        fov=40), shapes=[quad]))
+    qn, qt, _ = capi.build_bvh_host(qs.vertices, qs.indices)
+    qo = O.OracleScene(qs, qn, qt, capi)
+    r, w, _ = qo.render_ao(3)
+    assert np.all(r == 3)
+
+
 SDL = """
 // a scene written in the reference's language (core/parser.cpp:150-363)
 let grey = [0.725, 0.71, 0.68]
