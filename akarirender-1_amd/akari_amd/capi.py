@@ -124,6 +124,7 @@ EXPORTS = {
     "akr_hip_trace_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_int, _P]),
     "akr_hip_render": (C.c_int, [_P, C.POINTER(PtParams), _P, C.c_int32, _P, _P]),
     "akr_hip_render_ao": (C.c_int, [_P, C.POINTER(AoParams), _P, C.c_int32, _P, _P]),
+    "akr_hip_ray_steps": (C.c_int, [_P, _P, C.c_uint64]),
     "akr_hip_render_device": (C.c_int, [_P, C.POINTER(PtParams), _P, C.c_int32, _P, _P, _P,
                                         C.POINTER(C.c_uint64)]),
     "akr_hip_kernel_stats": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
@@ -373,6 +374,12 @@ class HipContext:
                                                    C.c_void_p(d_radiance), C.c_void_p(d_weight), C.c_void_p(stream),
                                                    C.byref(npx)))
         return npx.value
+
+    def ray_steps(self, n: int) -> np.ndarray:
+        """Per-ray traversal iterations of the last standalone trace (option "ray_steps")."""
+        out = np.zeros(n, np.uint32)
+        self._check(self.lib.akr_hip_ray_steps(self.h, _ptr(out), n))
+        return out
 
     def kernel_stats(self) -> dict:
         n = C.c_int32(0)

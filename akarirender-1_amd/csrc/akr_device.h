@@ -108,6 +108,7 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
                                    // (3 x float4 each); wide leaf refs hold the float4 offset
     uint32_t wide_root;            // wide reference of the real root
     TraceCounters *counters;       // [3]: closest, any, shadow
+    uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
 };
 
 struct ShadeArgs {

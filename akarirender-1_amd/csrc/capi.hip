@@ -203,6 +203,9 @@ struct akr_hip_ctx {
     bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
     int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
+    bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
+    DBuf<uint32_t> d_steps;
+    uint64_t n_steps = 0;
     DBuf<TraceCounters> d_counters;
     std::vector<hipEvent_t> pool;
     struct Pending {
@@ -452,7 +455,7 @@ struct akr_hip_ctx {
         if (!accel_built) throw std::runtime_error("acceleration structure not built (call akr_hip_build_accel)");
         commit_scene();
         ensure_trace_grid();
-        if (count) {
+        if (count || ray_steps) {
             if (!d_counters.p) {
                 d_counters.reserve(3);
                 HIPCHK(hipMemset(d_counters.p, 0, 3 * sizeof(TraceCounters)));
@@ -469,7 +472,15 @@ struct akr_hip_ctx {
         t.n = (uint32_t)n;
         t.abi_hits = hits;
         int mode = any ? TRACE_ANY : TRACE_CLOSEST;
-        timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, st); });
+        if (ray_steps) {
+            d_steps.reserve(n);
+            n_steps = n;
+            t.ray_steps = d_steps.p;
+            timed(any ? "trace_any" : "trace_closest", st,
+                  [&] { launch_trace(mode, true, !exact_cull, wide, t, grid_for(mode, n), st); });
+        } else {
+            timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, st); });
+        }
         HIPCHK(hipGetLastError());
     }
 
@@ -749,6 +760,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->exact_cull = value != 0;
         } else if (k == "count_tests") {
             ctx->count = value != 0;
+        } else if (k == "ray_steps") {
+            ctx->ray_steps = value != 0;
         } else if (k == "wide") {
             ctx->wide = value != 0;
         } else if (k == "rays_per_lane") {
@@ -1097,6 +1110,16 @@ int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, ui
 }
 const void *akr_bvh_host_wide_nodes(const akr_bvh_host *h) { return h ? h->wide.nodes.data() : nullptr; }
 const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h) { return h ? h->wide.leaves.data() : nullptr; }
+
+int akr_hip_ray_steps(akr_hip_ctx *ctx, uint32_t *out, uint64_t n) {
+    return guard(ctx, [&] {
+        if (!ctx->ray_steps || n > ctx->n_steps) throw std::runtime_error("no per-ray steps recorded for that many rays");
+        if (n == 0) return;
+        if (!out) throw std::runtime_error("null output");
+        HIPCHK(hipMemcpyAsync(out, ctx->d_steps.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    });
+}
 
 int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n) {
     return guard(ctx, [&] {

@@ -401,6 +401,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     float tmin = 0.0f, tmax = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
     uint32_t bgid = kNoHit, idx = 0, cur = AKR_CHILD_EMPTY, leaf = AKR_CHILD_EMPTY;
     int sp = 0;
+    uint32_t steps = 0;  // COUNT only (ray_steps diagnostic)
     bool busy = false, occluded = false, drained = n == 0;
     // The queue [0, n) is cut into kWorkShards contiguous ranges, each with its own counter on its
     // own 128-B line: one counter word saturates at ~88 returning atomics/us chip-wide, so a
@@ -461,6 +462,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 if (COUNT) {
                     c_strav++;  // every lane of the (converged) wave
                     c_sleaf += busy ? 1 : 0;
+                    steps += busy ? 1 : 0;
                 }
                 if (WIDE && busy && is_internal(cur)) {
                     const int nt = visit_wide<TIGHT, ANY>(wn, cur, o, d, invd, tmin, tmax, best, s_stack, stack_ovf,
@@ -519,7 +521,10 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                     const float4 ta = k == 0 ? pa : tp[3 * k + 0];
                     const float4 tb = k == 0 ? pb : tp[3 * k + 1];
                     const float4 tc = k == 0 ? pc : tp[3 * k + 2];
-                    if (COUNT) c_tri++;
+                    if (COUNT) {
+                        c_tri++;
+                        steps++;
+                    }
                     float t, u, v;
                     if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
                         best = t;
@@ -537,6 +542,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             if (busy && ((ANY && occluded) || cur == AKR_CHILD_EMPTY)) {
                 busy = false;
                 emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
+                if (COUNT && a.ray_steps) a.ray_steps[idx] = steps;
             }
         }
         if (fresh) {
@@ -548,6 +554,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             if (WIDE && !fast_box_ok(o, invd, tmin, tmax)) {  // rare: exact BVH2 traversal, inline
                 if (COUNT) c_rays++;
                 trace_exact_lane<MODE, TIGHT>(a, idx, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid);
+                if (COUNT && a.ray_steps) a.ray_steps[idx] = 0xFFFFFFFFu;  // traced outside the wide loop
                 fresh = false;
             }
         }
@@ -558,7 +565,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             occluded = false;
             sp = 0;
             leaf = AKR_CHILD_EMPTY;
-            if (COUNT) { c_rays++; c_box++; }
+            if (COUNT) { c_rays++; c_box++; steps = 0; }
             const float tr = box_test<TIGHT, WIDE>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
             cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
             busy = true;

@@ -245,6 +245,11 @@ int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, 
 int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
 int akr_hip_synchronize(akr_hip_ctx *ctx);
+/* Diagnostic: with option "ray_steps" set, each standalone trace (akr_hip_trace /
+ * akr_hip_trace_device) runs the counting kernel and records, per ray, the traversal-loop
+ * iterations it was active for plus its triangle tests (0xFFFFFFFF: traced by the exact BVH2
+ * fallback); this copies the first n of the last trace to host memory. */
+int akr_hip_ray_steps(akr_hip_ctx *ctx, uint32_t *out, uint64_t n);
 
 #ifdef __cplusplus
 }

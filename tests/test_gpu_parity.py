@@ -289,3 +289,37 @@ def test_render_ao_edges(hip_ctx_factory):
         assert not w.any()
         # the path tracer after AO on the same context still matches its oracle
         _check_render(ctx, orc, 2, 5, tiles, 40, 24)
+
+
+def test_scene_file_render_ao_and_path(tmp_path):
+    """SceneNode::render on the HIP path (akari_amd.render): a .akari scene with an AO node, then
+    a Path node, each through its C-ABI integrator, the AO image bit-exact against the oracle."""
+    from akari_amd import film, render
+    from conftest import CORNELL_MESH
+    sdl = f"""
+let grey = DiffuseMaterial {{ color: [0.725, 0.71, 0.68] }}
+export scene = Scene {{
+    camera: PerspectiveCamera {{ fov: 15, position: [0, 1, 9], resolution: [40, 24] }},
+    integrator: AO {{ spp: 5, occlude: 0.75 }},
+    output: "{tmp_path / 'ao.pfm'}",
+    shapes: [ AkariMesh {{ path: "{CORNELL_MESH}", materials: [$grey, $grey, $grey, $grey, $grey, $grey, $grey,
+                                                                 EmissiveMaterial {{ color: [17, 12, 4] }}] }} ]
+}}
+"""
+    path = tmp_path / "ao.akari"
+    path.write_text(sdl)
+    assert render.main([str(path)]) == 0
+    raw = (tmp_path / "ao.pfm").read_bytes()
+    img = np.frombuffer(raw[raw.index(b"-1.0\n") + 5:], np.float32).reshape(24, 40, 3)[::-1]
+    sc = scene.load_scene_file(path)
+    cs = scene.compile_scene(sc)
+    with capi.HipContext(0) as ctx:
+        scene.upload_scene(ctx, cs)
+        nodes, tris = ctx.accel_export()
+    orc = py_oracle.OracleScene(cs, nodes, tris, capi)
+    orad, ow, _ = orc.render_ao(5, occlude=np.float32(0.75))
+    assert np.array_equal(img, film.resolve(orad, ow))
+    path.write_text(sdl.replace("AO { spp: 5, occlude: 0.75 }", "Path { spp: 3, max_depth: 4, tile_size: 16 }"))
+    rad, w = render.render_scene(scene.load_scene_file(path))
+    orad, ow, _ = orc.render(3, 4, tiles=render._tiles(sc, 16), ray_clamp=10.0)
+    assert np.array_equal(rad, orad) and np.array_equal(w, ow)

@@ -290,3 +290,13 @@ def test_soup_scene_lights():
     assert ng[1] < 0                      # one-sided emitter facing -y (light.h:67)
     # power = |cross| (twice the area: 4) * texcoord area (0.5) * luminance (10), scene.cpp:72-87
     assert np.allclose(cs.power, 4 * 0.5 * 10, rtol=1e-6)
+
+
+def test_render_scene_fails_loudly_without_gpu(tmp_path):
+    """No CPU fallback: the scene renderer goes through the HIP library or raises."""
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from akari_amd import render
+    with pytest.raises(capi.AkrError):
+        render.render_scene(cornell((8, 8)))
