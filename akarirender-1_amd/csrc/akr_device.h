@@ -31,6 +31,10 @@ constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once a
 #define AKR_WHILE_EXIT 16
 #endif
 constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
+#ifndef AKR_LEAF_PREFETCH
+#define AKR_LEAF_PREFETCH 0
+#endif
+constexpr bool kLeafPrefetch = AKR_LEAF_PREFETCH != 0;  // load a leaf's blob when it is found, not in the leaf phase
 #ifndef AKR_WORK_SHARDS
 #define AKR_WORK_SHARDS 8
 #endif
@@ -107,6 +111,7 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     const float4 *wide_leaves;     // leaf blob: per leaf [lo.xyz hi.x | hi.yz first count] + its triangles
                                    // (3 x float4 each); wide leaf refs hold the float4 offset
     uint32_t wide_root;            // wide reference of the real root
+    uint32_t lean;                 // 1: lean slot tests allowed (wide view's frames bounded by 2^40)
     TraceCounters *counters;       // [3]: closest, any, shadow
     uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
 };

@@ -43,6 +43,7 @@ struct Bvh4Output {
     std::vector<akr_bvh_leaf> leaves;
     uint32_t root_ref = AKR_CHILD_EMPTY;
     int max_depth = 0;
+    float max_abs = 0.0f;  // largest |frame origin| and frame step 2^e over all wide nodes (lean test bound)
 };
 
 void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out);

@@ -3,14 +3,31 @@
 //
 // Each wide node is a BVH2 node with its two children folded in, so a traversal step replaces
 // two BVH2 levels and fetches 64 B for four child boxes instead of 2 x 64 B.  Correctness does
-// not rest on the quantized boxes: they only have to CONTAIN the exact ones (checked here with
-// the device's own fmaf arithmetic), and every leaf is re-tested with its exact box.
+// not rest on the quantized boxes: they only have to CONTAIN the exact ones (checked here in real
+// arithmetic, which implies the device's fmaf decode), and every leaf is re-tested with its exact box.
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include "bvh_build.h"
 
 namespace akr {
+
+// The quantized bound must lie outside the exact one in REAL arithmetic (origin + q * s, no
+// rounding), not only after the device's fmaf rounding: the lean slot test (kernels.hip
+// visit_wide_lean) folds origin and q * s into one fma per bound with an error slack derived for
+// the real value.  Real containment implies the fmaf one (rounding is monotone and `bound` is a
+// float).  The real value is evaluated in long double with a margin that covers its own rounding.
+static bool real_le(uint32_t q, float s, float origin, float bound) {
+    const long double v = (long double)origin + (long double)q * (long double)s;
+    const long double m = std::ldexp(1.0L, -60) * (std::fabs((long double)origin) + 255.0L * s + std::fabs((long double)bound));
+    return v + m <= (long double)bound;
+}
+
+static bool real_ge(uint32_t q, float s, float origin, float bound) {
+    const long double v = (long double)origin + (long double)q * (long double)s;
+    const long double m = std::ldexp(1.0L, -60) * (std::fabs((long double)origin) + 255.0L * s + std::fabs((long double)bound));
+    return v - m >= (long double)bound;
+}
 
 namespace {
 
@@ -108,8 +125,10 @@ struct Collapser {
                 e = std::max(-126, k - 1);
             }
             while (e < 127 && 255.0 * std::ldexp(1.0, e) < ext) e++;
-            while (e < 127 && std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k]) e++;
-            if (std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k]) throw std::runtime_error("BVH bounds too large to quantize");
+            while (e < 127 && (std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k] || !real_ge(255, pow2f(e), plo[k], phi[k]))) e++;
+            if (std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k] || !real_ge(255, pow2f(e), plo[k], phi[k]))
+                throw std::runtime_error("BVH bounds too large to quantize");
+            out.max_abs = std::max(out.max_abs, std::max(std::fabs(plo[k]), pow2f(e)));
             ex[k] = (uint32_t)(e + 127);
         }
         w.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | (axis[0] | axis[1] << 2 | axis[2] << 4) << 24;
@@ -142,17 +161,19 @@ uint32_t quantize_lo(float bound, float origin, float s) {
     double q = std::floor(((double)bound - (double)origin) / (double)s);
     q = std::min(255.0, std::max(0.0, q));
     uint32_t qi = (uint32_t)q;
-    while (qi > 0 && std::fmaf((float)qi, s, origin) > bound) qi--;
-    if (std::fmaf((float)qi, s, origin) > bound) throw std::runtime_error("quantize_lo: bound below origin");
-    return qi;
+    while (qi > 0 && (std::fmaf((float)qi, s, origin) > bound || !real_le(qi, s, origin, bound))) qi--;
+    if (std::fmaf((float)qi, s, origin) > bound || (qi > 0 && !real_le(qi, s, origin, bound)))
+        throw std::runtime_error("quantize_lo: bound below origin");
+    return qi;  // q = 0 is the origin itself, which is <= every bound of the frame
 }
 
 uint32_t quantize_hi(float bound, float origin, float s) {
     double q = std::ceil(((double)bound - (double)origin) / (double)s);
     q = std::min(255.0, std::max(0.0, q));
     uint32_t qi = (uint32_t)q;
-    while (qi < 255 && std::fmaf((float)qi, s, origin) < bound) qi++;
-    if (std::fmaf((float)qi, s, origin) < bound) throw std::runtime_error("quantize_hi: bound beyond the frame");
+    while (qi < 255 && (std::fmaf((float)qi, s, origin) < bound || !real_ge(qi, s, origin, bound))) qi++;
+    if (std::fmaf((float)qi, s, origin) < bound || !real_ge(qi, s, origin, bound))
+        throw std::runtime_error("quantize_hi: bound beyond the frame");
     return qi;
 }
 
@@ -160,6 +181,7 @@ void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out) {
     out.nodes.clear();
     out.leaves.clear();
     out.max_depth = 0;
+    out.max_abs = 0.0f;
     out.root_ref = AKR_CHILD_EMPTY;
     if (bvh2.empty()) return;
     const akr_bvh_node &vroot = bvh2[0];  // virtual root: child 0 = the real root

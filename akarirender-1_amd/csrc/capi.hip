@@ -203,6 +203,7 @@ struct akr_hip_ctx {
     bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
     int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
+    bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
     bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
     DBuf<uint32_t> d_steps;
     uint64_t n_steps = 0;
@@ -441,6 +442,8 @@ struct akr_hip_ctx {
         t.wide_nodes = reinterpret_cast<const float4 *>(d_wnodes.p);
         t.wide_leaves = reinterpret_cast<const float4 *>(d_wleaves.p);
         t.wide_root = wide_root_dev;
+        // the lean slot test's slack is derived for frame origins and steps below 2^40
+        t.lean = lean && bvh4.max_abs <= 0x1p40f ? 1u : 0u;
         t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
@@ -764,6 +767,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->ray_steps = value != 0;
         } else if (k == "wide") {
             ctx->wide = value != 0;
+        } else if (k == "lean") {
+            ctx->lean = value != 0;
         } else if (k == "rays_per_lane") {
             if (value < 1 || value > 64) throw std::runtime_error("rays_per_lane must be in [1, 64]");
             ctx->rays_per_lane = (int)value;

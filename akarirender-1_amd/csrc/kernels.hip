@@ -207,8 +207,52 @@ __device__ __forceinline__ float ubyte(uint32_t w, int k) {  // v_cvt_f32_ubyte{
     return (float)((w >> (8 * k)) & 0xFFu);
 }
 
+// Continue with the first entered slot of a wide node in the BVH2 depth-first order and push the
+// other entered slots behind it, each with its entry distance; pop when no slot is entered.
+// `dpos` holds the ray's direction signs: bit a = (d[a] > 0).  The order is a permutation of the
+// slots by three flip bits (near = left iff d[axis] > 0 at each of the three folded BVH2 nodes):
+// position(slot k) = k ^ (f0 << 1 | f_{1 + k/2}).  Entered slots are ranked by position without
+// moving any data: the first becomes `cur`, each other one is written straight to its stack entry
+// sp + (number of entered slots at later positions), so the earliest is popped first.
+template <bool ANY>
+__device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, const float (&t)[4], const bool (&hit)[4],
+                                                const uint32_t (&ref)[4], uint32_t &cur, float lim, lds_u64 *s_stack,
+                                                glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
+                                                int &sp) {
+    const uint32_t ax = meta >> 24;
+    const uint32_t f0 = ~(dpos >> (ax & 3u)) & 1u;
+    const uint32_t f1 = ~(dpos >> ((ax >> 2) & 3u)) & 1u;
+    const uint32_t f2 = ~(dpos >> ((ax >> 4) & 3u)) & 1u;
+    const uint32_t m01 = (f0 << 1) | f1, m23 = (f0 << 1) | f2;
+    const uint32_t pos[4] = {m01, 1u ^ m01, 2u ^ m23, 3u ^ m23};
+    uint32_t pm = 0;  // entered slots, by position
+#pragma unroll
+    for (int k = 0; k < 4; k++) pm |= hit[k] ? (1u << pos[k]) : 0u;
+    if (pm == 0) {
+        cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim);
+        return;
+    }
+    const uint32_t rest = pm & (pm - 1u);  // entered slots after the first: pushed
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if ((rest >> pos[k]) & 1u) {
+            const int e = sp + (int)__popc(rest >> (pos[k] + 1u));
+            const unsigned long long v = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
+            if (e < kStackLds) s_stack[e * kBlock + tid] = v;
+            else ovf[(size_t)(e - kStackLds) * ovf_threads + gtid] = v;
+        }
+    }
+    sp += (int)__popc(rest);
+    // the slot at the first entered position (selects on static indices: no private array)
+    const uint32_t first = pm ^ rest;
+    uint32_t c = AKR_CHILD_EMPTY;
+#pragma unroll
+    for (int k = 0; k < 4; k++) c = ((first >> pos[k]) & 1u) ? ref[k] : c;
+    cur = c;
+}
+
 template <bool TIGHT, bool ANY>
-__device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o, V3 d, V3 invd, float tmin, float tmax,
+__device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o, uint32_t dpos, V3 invd, float tmin, float tmax,
                                           float best, lds_u64 *s_stack, glb_u64 *ovf, uint32_t ovf_threads,
                                           uint32_t tid, uint32_t gtid, int &sp) {
     const uint4 *wu = reinterpret_cast<const uint4 *>(wn);
@@ -235,44 +279,91 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    // BVH2 depth-first order: at each of the three folded nodes, near = left iff d[axis] > 0
-    const uint32_t ax = meta >> 24;
-    const float d0 = (ax & 3u) == 0 ? d.x : ((ax & 3u) == 1 ? d.y : d.z);
-    const float d1 = ((ax >> 2) & 3u) == 0 ? d.x : (((ax >> 2) & 3u) == 1 ? d.y : d.z);
-    const float d2 = ((ax >> 4) & 3u) == 0 ? d.x : (((ax >> 4) & 3u) == 1 ? d.y : d.z);
-    auto swap_slots = [&](bool sw, int i, int j) {
-        const float ti = t[i];
-        const bool hi_ = hit[i];
-        const uint32_t ri = ref[i];
-        t[i] = sw ? t[j] : ti;
-        hit[i] = sw ? hit[j] : hi_;
-        ref[i] = sw ? ref[j] : ri;
-        t[j] = sw ? ti : t[j];
-        hit[j] = sw ? hi_ : hit[j];
-        ref[j] = sw ? ri : ref[j];
-    };
-    swap_slots(!(d1 > 0), 0, 1);
-    swap_slots(!(d2 > 0), 2, 3);
-    const bool swp = !(d0 > 0);
-    swap_slots(swp, 0, 2);
-    swap_slots(swp, 1, 3);
-    uint32_t cand = AKR_CHILD_EMPTY;
-    float tc = 0.0f;
-#pragma unroll
-    for (int k = 3; k >= 0; k--) {
-        if (hit[k]) {
-            if (cand != AKR_CHILD_EMPTY) {
-                const unsigned long long e = (unsigned long long)cand | ((unsigned long long)__float_as_uint(tc) << 32);
-                if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
-                else ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid] = e;
-                sp++;
-            }
-            cand = ref[k];
-            tc = t[k];
-        }
-    }
-    cur = cand != AKR_CHILD_EMPTY ? cand : stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim);
+    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, lim, s_stack, ovf, ovf_threads, tid, gtid, sp);
     return tested;
+}
+
+// Lean slot test ("lean slot test"): the same conservative test in fewer VALU
+// operations.  Per node and axis it forms oq = (origin - o) * invd and sc = 2^e * invd (exact), and
+// per slot bound one fma: q * sc + oq is (bound - o) * invd in real arithmetic.  An error slack
+// E = 8u * (|oq| + 255 |sc|) + 2^-120 (u = 2^-24), folded into oq once per node (oq - E for the
+// entry side, oq + E for the exit side), makes the per-axis entry value <= and the exit value >=
+// the reference's RN(RN(b - o) * invd) for the exact BVH2 box (the builder quantizes outward in
+// real arithmetic, bvh_wide.cpp).  Entry and exit bounds are chosen per node from the sign of invd
+// instead of a min/max per slot.  So the test passes whenever the exact one does, with an entry
+// distance no larger: leaves are still reached, in order, and re-tested exactly.  Only for rays
+// with `lean_ok` (fast_box_ok, tmin >= 0, |o| <= 2^60, |invd| <= 2^64) on a wide view whose frame
+// origins and steps are <= 2^40, which bounds every term below 2^126 (no overflow, no NaN); with
+// tmin >= 0 the reference's "t < 0" reject cannot fire and TIGHT's t <= m1 implies m0 <= m1, and
+// t < tmax is t <= tmaxp (the float below tmax).
+template <bool ANY>
+__device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, V3 o, uint32_t dpos, V3 invd, float tmin,
+                                               float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
+                                               uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
+    const uint4 *wu = reinterpret_cast<const uint4 *>(wn);
+    const float4 h = wn[4 * (size_t)cur + 0];
+    const uint4 c = wu[4 * (size_t)cur + 1];
+    const uint4 qa = wu[4 * (size_t)cur + 2];
+    const uint4 qb = wu[4 * (size_t)cur + 3];
+    uint32_t meta = __float_as_uint(h.w);
+#ifdef AKR_PROBE_EXTRA_VALU  // bottleneck probe only: ~AKR_PROBE_EXTRA_VALU dependent VALU ops per visit
+    {
+        float x = h.x;
+        for (int k = 0; k < AKR_PROBE_EXTRA_VALU; k++) {
+            x = x * 1.0001f;
+            asm volatile("" : "+v"(x));
+        }
+        meta |= __float_as_uint(x) & 0u;
+        asm volatile("" : "+v"(meta));
+    }
+#endif
+    constexpr float kRel = 0x1p-21f;   // 8u
+    constexpr float kAbs = 0x1p-120f;  // covers an underflowing sc
+    const float scx = __uint_as_float((meta & 0xFFu) << 23) * invd.x;
+    const float scy = __uint_as_float(((meta >> 8) & 0xFFu) << 23) * invd.y;
+    const float scz = __uint_as_float(((meta >> 16) & 0xFFu) << 23) * invd.z;
+    const float oqx = (h.x - o.x) * invd.x, oqy = (h.y - o.y) * invd.y, oqz = (h.z - o.z) * invd.z;
+    const float ex = __builtin_fmaf(__builtin_fmaf(255.0f, fabsf(scx), fabsf(oqx)), kRel, kAbs);
+    const float ey = __builtin_fmaf(__builtin_fmaf(255.0f, fabsf(scy), fabsf(oqy)), kRel, kAbs);
+    const float ez = __builtin_fmaf(__builtin_fmaf(255.0f, fabsf(scz), fabsf(oqz)), kRel, kAbs);
+    const float nox = oqx - ex, noy = oqy - ey, noz = oqz - ez;  // entry side
+    const float fox = oqx + ex, foy = oqy + ey, foz = oqz + ez;  // exit side
+    const bool px = invd.x > 0.0f, py = invd.y > 0.0f, pz = invd.z > 0.0f;
+    const uint32_t qnx = px ? qa.x : qa.y, qfx = px ? qa.y : qa.x;
+    const uint32_t qny = py ? qa.z : qa.w, qfy = py ? qa.w : qa.z;
+    const uint32_t qnz = pz ? qb.x : qb.y, qfz = pz ? qb.y : qb.x;
+    const float lim = ANY ? tmaxp : fminf(best, tmaxp);
+    float t[4];
+    bool hit[4];
+    uint32_t ref[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float nx = __builtin_fmaf(ubyte(qnx, k), scx, nox), fx = __builtin_fmaf(ubyte(qfx, k), scx, fox);
+        const float ny = __builtin_fmaf(ubyte(qny, k), scy, noy), fy = __builtin_fmaf(ubyte(qfy, k), scy, foy);
+        const float nz = __builtin_fmaf(ubyte(qnz, k), scz, noz), fz = __builtin_fmaf(ubyte(qfz, k), scz, foz);
+        const float tk = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
+        const float m1 = fminf(fminf(fx, fy), fminf(fz, lim));
+        t[k] = tk;
+        hit[k] = ref[k] != AKR_CHILD_EMPTY && tk <= m1;
+    }
+    const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
+                       (c.w != AKR_CHILD_EMPTY);
+    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid, sp);
+    return tested;
+}
+
+// The float just below `x` (x not NaN): t < x  <=>  t <= below(x) for every float t.
+__device__ __forceinline__ float float_below(float x) {
+    const uint32_t b = __float_as_uint(x);
+    if (x > 0.0f) return __uint_as_float(b - 1u);
+    if (x == 0.0f) return -0x1p-149f;
+    return __uint_as_float(b + 1u);  // negative (incl. -inf -> NaN never: -inf has no float below)
+}
+
+__device__ __forceinline__ bool lean_ok(V3 o, V3 invd, float tmin, float tmax) {
+    const float mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float mi = fmaxf(fmaxf(fabsf(invd.x), fabsf(invd.y)), fabsf(invd.z));
+    return fast_box_ok(o, invd, tmin, tmax) && tmin >= 0.0f && tmax > -INFINITY && mo <= 0x1p60f && mi <= 0x1p64f;
 }
 
 // Result of one finished ray: the closest hit (float4 queue record or akr_hit), or for a shadow
@@ -374,10 +465,11 @@ __device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t id
 // box tests but never a different hit.  A node's two child boxes are tested when the node is
 // visited and the far child is pushed with its entry distance, re-compared against the current
 // best when popped — the reference's pop-time test of the node's own box.
-// Registers are capped for 6 waves per SIMD (<= 80 VGPRs), which the LDS stack allows anyway
-// (6 x 24 KB workgroups per CU); uncapped, the inlined exact-lane path pushes the kernel to 85.
+// Registers are capped for 5 waves per SIMD (<= 96 VGPRs; the LDS stack allows 6 workgroups of
+// 4 waves per CU): at the 6-wave cap (80 VGPRs) the kernel spills and the closest-hit launch is
+// 4 % slower, the small (8-way split) launches 5 % slower.
 #ifndef AKR_TRACE_WAVES
-#define AKR_TRACE_WAVES 6
+#define AKR_TRACE_WAVES 5
 #endif
 #define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
 template <int MODE, bool COUNT, bool TIGHT, bool WIDE>
@@ -398,11 +490,14 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0, c_visit = 0;
 
     V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
-    float tmin = 0.0f, tmax = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
+    float tmin = 0.0f, tmax = 0.0f, tmaxp = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
+    bool lean = false;  // this ray takes the lean slot test (visit_wide_lean)
+    uint32_t dpos = 0;  // direction signs: bit a = (d[a] > 0)
     uint32_t bgid = kNoHit, idx = 0, cur = AKR_CHILD_EMPTY, leaf = AKR_CHILD_EMPTY;
     int sp = 0;
     uint32_t steps = 0;  // COUNT only (ray_steps diagnostic)
     bool busy = false, occluded = false, drained = n == 0;
+    float4 lq0 = {}, lq1 = {}, lqa = {}, lqb = {}, lqc = {};  // prefetched blob of the pending leaf
     // The queue [0, n) is cut into kWorkShards contiguous ranges, each with its own counter on its
     // own 128-B line: one counter word saturates at ~88 returning atomics/us chip-wide, so a
     // single shared counter capped the refill rate.  A wave starts on shard blockIdx % 8 (the
@@ -465,8 +560,13 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                     steps += busy ? 1 : 0;
                 }
                 if (WIDE && busy && is_internal(cur)) {
-                    const int nt = visit_wide<TIGHT, ANY>(wn, cur, o, d, invd, tmin, tmax, best, s_stack, stack_ovf,
-                                                          a.ovf_threads, tid, gtid, sp);
+                    int nt;
+                    if (TIGHT && lean)
+                        nt = visit_wide_lean<ANY>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
+                                                  a.ovf_threads, tid, gtid, sp);
+                    else
+                        nt = visit_wide<TIGHT, ANY>(wn, cur, o, dpos, invd, tmin, tmax, best, s_stack, stack_ovf,
+                                                    a.ovf_threads, tid, gtid, sp);
                     if (COUNT) {
                         c_box += nt;
                         c_visit++;
@@ -485,6 +585,16 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 }
                 if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
                     leaf = cur;  // postpone the leaf and keep descending
+                    if (WIDE && kLeafPrefetch) {
+                        // issue the leaf blob's loads now: they complete under the speculative
+                        // node visits below instead of adding one dependent fetch to the leaf phase
+                        const float4 *lr = a.wide_leaves + (leaf & 0x7FFFFFFFu);
+                        lq0 = lr[0];
+                        lq1 = lr[1];
+                        lqa = lr[2];
+                        lqb = lr[3];
+                        lqc = lr[4];
+                    }
                     cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
                 }
                 // leave for the leaf phase once at most kWhileExit lanes are still searching for
@@ -500,10 +610,20 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 float4 pa, pb, pc;  // the first one, fetched together with the leaf header
                 if (WIDE) {  // the leaf's exact box, with the current best: the BVH2 pop-time test
                     const float4 *lr = a.wide_leaves + (leaf & 0x7FFFFFFFu);
-                    const float4 l0 = lr[0], l1 = lr[1];  // lo.xyz hi.x | hi.yz first count
-                    pa = lr[2];
-                    pb = lr[3];
-                    pc = lr[4];
+                    float4 l0, l1;  // lo.xyz hi.x | hi.yz first count
+                    if (kLeafPrefetch) {
+                        l0 = lq0;
+                        l1 = lq1;
+                        pa = lqa;
+                        pb = lqb;
+                        pc = lqc;
+                    } else {
+                        l0 = lr[0];
+                        l1 = lr[1];
+                        pa = lr[2];
+                        pb = lr[3];
+                        pc = lr[4];
+                    }
                     const float tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
                     const bool in = !(tl < 0.0f || tl > (ANY ? tmax : best));
                     if (COUNT) c_box++;
@@ -551,6 +671,11 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             tmin = ra.w;
             tmax = rb.w;
             invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
+            if (WIDE && TIGHT) {
+                lean = a.lean && lean_ok(o, invd, tmin, tmax);
+                tmaxp = float_below(tmax);
+            }
             if (WIDE && !fast_box_ok(o, invd, tmin, tmax)) {  // rare: exact BVH2 traversal, inline
                 if (COUNT) c_rays++;
                 trace_exact_lane<MODE, TIGHT>(a, idx, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid);

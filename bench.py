@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=1)
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
+    ap.add_argument("--lean", type=int, default=1, help="lean slot tests in the wide traversal (0: reference arithmetic)")
     ap.add_argument("--timed-stats", type=int, default=1,
                     help="per-kernel HIP events inside the timed region (0: probe their overhead)")
     ap.add_argument("--emulate-world", type=int, default=0,
@@ -106,6 +107,8 @@ def main():
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)
+    if not args.lean:
+        ctx.set_option("lean", 0)
     log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 

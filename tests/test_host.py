@@ -300,3 +300,126 @@ def test_render_scene_fails_loudly_without_gpu(tmp_path):
     from akari_amd import render
     with pytest.raises(capi.AkrError):
         render.render_scene(cornell((8, 8)))
+
+
+def _f32_fma(a, b, c):
+    """f32 fma emulated in f64: exact whenever a * b + c fits 53 bits (always here: 8-bit q or
+    255 times a 24-bit float, plus a 24-bit float within 2^29 of it), then one rounding."""
+    return (np.float64(a) * np.float64(b) + np.float64(c)).astype(np.float32)
+
+
+def _lean_slot_test(node, slot, o, invd, tmin, lim):
+    """kernels.hip visit_wide_lean for one slot, emulated in f32 (vectorised over rays)."""
+    f = np.float32
+    meta = int(node["meta"])
+    s = np.array([np.float32(2.0 ** (((meta >> (8 * a)) & 0xFF) - 127)) for a in range(3)], np.float32)
+    sc = (s[None, :] * invd).astype(f)
+    oq = ((node["origin"][None, :].astype(f) - o).astype(f) * invd).astype(f)
+    e = _f32_fma(_f32_fma(f(255.0), np.abs(sc), np.abs(oq)), f(2.0 ** -21), f(2.0 ** -120))
+    no, fo = (oq - e).astype(f), (oq + e).astype(f)
+    q = [[(int(node["q"][2 * a + hi]) >> (8 * slot)) & 0xFF for hi in (0, 1)] for a in range(3)]
+    pos = invd > 0
+    qn = np.stack([np.where(pos[:, a], q[a][0], q[a][1]) for a in range(3)], 1).astype(f)
+    qf = np.stack([np.where(pos[:, a], q[a][1], q[a][0]) for a in range(3)], 1).astype(f)
+    n = _f32_fma(qn, sc, no)
+    x = _f32_fma(qf, sc, fo)
+    t = np.maximum(n.max(1), tmin)
+    m1 = np.minimum(x.min(1), lim)
+    return t <= m1, t
+
+
+def _ref_box_test(lo, hi, o, invd, tmin, tmax, best):
+    """The reference intersectAABB (bvh-accelerator.h:89-103) with the tight cull and the
+    traversal's cull (t < 0 or t > best), in f32."""
+    t0 = ((lo[None, :] - o).astype(np.float32) * invd).astype(np.float32)
+    t1 = ((hi[None, :] - o).astype(np.float32) * invd).astype(np.float32)
+    m0 = np.minimum(t0, t1).max(1)
+    m1 = np.maximum(t0, t1).min(1)
+    t = np.maximum(tmin, m0)
+    hit = (m0 <= m1) & (t < tmax) & (t <= m1) & ~(t < 0) & ~(t > best)
+    return hit, t
+
+
+def test_lean_slot_test_conservative():
+    """The lean slot test passes whenever the reference test of the exact box
+    passes, with an entry distance no larger — on every leaf slot of a built wide view, for
+    random rays and for rays aimed at each box's corners, edges and faces (grazing), with
+    bounded and unbounded intervals."""
+    cs = scene.compile_scene(small_soup(3_000))
+    _, _, _, wide = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=1, wide=True)
+    wn, lv, _ = wide
+    rng = np.random.default_rng(5)
+    base = random_rays(512, 3, -1.3, 1.3)
+    checked = 0
+    for ni in range(len(wn)):
+        node = wn[ni]
+        for k in range(4):
+            c = int(node["child"][k])
+            if c == 0xFFFFFFFF or not (c & 0x80000000):
+                continue
+            leaf = lv[c & 0x7FFFFFFF]
+            # 48 rays through corner / edge / face points of this box at t = dist
+            m = 48
+            sel = rng.integers(0, 3, (m, 3))
+            tgt = np.where(sel == 0, leaf["lo"], np.where(sel == 1, leaf["hi"], (leaf["lo"] + leaf["hi"]) / 2))
+            dd = rng.normal(size=(m, 3)).astype(np.float32)
+            dd /= np.linalg.norm(dd, axis=1, keepdims=True).astype(np.float32)
+            dist = rng.choice(np.float32([0.01, 0.37, 3.0]), m).astype(np.float32)
+            o = np.concatenate([base["o"], (tgt - dd * dist[:, None]).astype(np.float32)]).astype(np.float32)
+            d = np.concatenate([base["d"], dd]).astype(np.float32)
+            invd = (np.float32(1.0) / d).astype(np.float32)
+            nr = o.shape[0]
+            tmin = rng.choice(np.float32([0.0, 1e-3, 0.2]), nr).astype(np.float32)
+            tmax = rng.choice(np.float32([np.inf, 0.37, 2.0]), nr).astype(np.float32)
+            best = rng.choice(np.float32([np.inf, 0.37, 1.0]), nr).astype(np.float32)
+            tmaxp = np.nextafter(tmax, np.float32(-np.inf)).astype(np.float32)
+            lim = np.minimum(best, tmaxp)
+            rh, rt = _ref_box_test(leaf["lo"], leaf["hi"], o, invd, tmin, tmax, best)
+            lh, lt = _lean_slot_test(node, k, o, invd, tmin, lim)
+            assert np.all(lh[rh]), f"lean test rejects a box the reference enters (node {ni}, slot {k})"
+            assert np.all(lt[rh] <= rt[rh])
+            checked += int(rh.sum())
+    assert checked > 20_000
+
+
+def test_lean_slot_test_conservative_on_grid_bounds():
+    """Adversarial boxes whose exact bounds lie ON the quantization grid (the builder's zero-slack
+    case): the lean test's per-axis values differ from the reference's by rounding only, which the
+    slack must cover.  Rays graze corners, edges and faces; magnitudes up to 2^20."""
+    rng = np.random.default_rng(11)
+    f = np.float32
+    n_box, m = 12000, 64
+    bad = 0
+    checked = 0
+    for b in range(n_box):
+        scale = f(2.0 ** rng.integers(-8, 20))
+        org = (rng.uniform(-1, 1, 3) * scale).astype(f)
+        e = rng.integers(-20, 12, 3) + int(np.log2(scale))
+        s = np.array([f(2.0 ** int(x)) for x in e], f)
+        q_lo = rng.integers(0, 128, 3)
+        q_hi = q_lo + rng.integers(0, 128, 3)
+        lo = (org.astype(np.float64) + q_lo * s.astype(np.float64))
+        hi = (org.astype(np.float64) + q_hi * s.astype(np.float64))
+        if np.any(lo.astype(f).astype(np.float64) != lo) or np.any(hi.astype(f).astype(np.float64) != hi):
+            continue  # keep boxes whose bounds are exactly on the grid
+        lo, hi = lo.astype(f), hi.astype(f)
+        node = np.zeros((), [("origin", f, 3), ("meta", np.uint32), ("q", np.uint32, 6)])
+        node["origin"] = org
+        node["meta"] = int(e[0] + 127) | int(e[1] + 127) << 8 | int(e[2] + 127) << 16
+        node["q"] = [int(q_lo[0]), int(q_hi[0]), int(q_lo[1]), int(q_hi[1]), int(q_lo[2]), int(q_hi[2])]
+        sel = rng.integers(0, 3, (m, 3))
+        tgt = np.where(sel == 0, lo, np.where(sel == 1, hi, ((lo + hi) / 2).astype(f))).astype(f)
+        d = rng.normal(size=(m, 3)).astype(f)
+        d[rng.random((m, 3)) < 0.2] *= f(1e-3)   # steep rays: large |invd|
+        d /= np.linalg.norm(d, axis=1, keepdims=True).astype(f)
+        dist = (rng.choice([0.01, 0.5, 7.0], m) * scale).astype(f)
+        o = (tgt - d * dist[:, None]).astype(f)
+        invd = (f(1.0) / d).astype(f)
+        tmin = np.zeros(m, f)
+        lim = np.full(m, np.finfo(f).max, f)
+        rh, rt = _ref_box_test(lo, hi, o, invd, tmin, np.full(m, np.inf, f), np.full(m, np.inf, f))
+        lh, lt = _lean_slot_test(node, 0, o, invd, tmin, lim)
+        bad += int(np.sum(rh & ~lh)) + int(np.sum(rh & (lt > rt)))
+        checked += int(rh.sum())
+    assert checked > 30_000
+    assert bad == 0
