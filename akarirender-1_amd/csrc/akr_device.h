@@ -31,15 +31,6 @@ constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once a
 #define AKR_WHILE_EXIT 16
 #endif
 constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
-#ifndef AKR_COOP
-#define AKR_COOP 0
-#endif
-constexpr bool kCoop = AKR_COOP != 0;     // cooperative tail traversal of closest-hit rays
-#define AKR_COOP_OFF 1u            // TraceArgs::coop: no cooperative tail
-#define AKR_COOP_FORCE_EXACT 2u    // every helper result takes the exact re-trace fallback (tests)
-#define AKR_COOP_HIT_ONLY 4u       // donate only once the donor has a hit (its stack entries then must be visited)
-                                   // bits 8+: minimum traversal iterations of a ray part before it donates
-constexpr int kMaxDonations = 5;          // per lane and ray part (6-bit helper lane ids in one u32)
 #ifndef AKR_WORK_SHARDS
 #define AKR_WORK_SHARDS 8
 #endif
@@ -117,7 +108,6 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
                                    // (3 x float4 each); wide leaf refs hold the float4 offset
     uint32_t wide_root;            // wide reference of the real root
     uint32_t lean;                 // 1: lean slot tests allowed (wide view's frames bounded by 2^40)
-    uint32_t coop;                 // AKR_COOP_* test/A-B switches of the cooperative tail
     TraceCounters *counters;       // [3]: closest, any, shadow
     uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
 };

@@ -204,7 +204,6 @@ struct akr_hip_ctx {
     int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
-    uint32_t coop = 0;        // AKR_COOP_* switches (option "coop")
     bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
     DBuf<uint32_t> d_steps;
     uint64_t n_steps = 0;
@@ -445,7 +444,6 @@ struct akr_hip_ctx {
         t.wide_root = wide_root_dev;
         // the lean slot test's slack is derived for frame origins and steps below 2^40
         t.lean = lean && bvh4.max_abs <= 0x1p40f ? 1u : 0u;
-        t.coop = coop;
         t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
@@ -771,14 +769,6 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->wide = value != 0;
         } else if (k == "lean") {
             ctx->lean = value != 0;
-        } else if (k == "coop") {  // 1 (default): cooperative tail; 0: off; 2: force its exact fallback
-            if (value < 0 || value > 2) throw std::runtime_error("coop must be 0, 1 or 2");
-            ctx->coop = (ctx->coop & ~3u) | (uint32_t)(value == 0 ? AKR_COOP_OFF : (value == 2 ? AKR_COOP_FORCE_EXACT : 0u));
-        } else if (k == "coop_hit_only") {
-            ctx->coop = value ? (ctx->coop | AKR_COOP_HIT_ONLY) : (ctx->coop & ~AKR_COOP_HIT_ONLY);
-        } else if (k == "coop_min_iters") {
-            if (value < 0 || value > 0xFFFFFF) throw std::runtime_error("coop_min_iters out of range");
-            ctx->coop = (ctx->coop & 0xFFu) | ((uint32_t)value << 8);
         } else if (k == "rays_per_lane") {
             if (value < 1 || value > 64) throw std::runtime_error("rays_per_lane must be in [1, 64]");
             ctx->rays_per_lane = (int)value;

@@ -139,8 +139,8 @@ typedef __attribute__((address_space(1))) unsigned long long glb_u64;
 // Pop the next stacked node whose stored entry distance is not beyond `lim` (the reference
 // re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
 __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_u64 *ovf, uint32_t ovf_threads,
-                                              uint32_t tid, uint32_t gtid, int &sp, float lim, int base = 0) {
-    while (sp > base) {  // entries below `base` were handed to helper lanes (cooperative tail)
+                                              uint32_t tid, uint32_t gtid, int &sp, float lim) {
+    while (sp > 0) {
         --sp;
         unsigned long long e;
         if (sp < kStackLds) e = s_stack[sp * kBlock + tid];
@@ -218,7 +218,7 @@ template <bool ANY>
 __device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, const float (&t)[4], const bool (&hit)[4],
                                                 const uint32_t (&ref)[4], uint32_t &cur, float lim, lds_u64 *s_stack,
                                                 glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
-                                                int &sp, int base = 0) {
+                                                int &sp) {
     const uint32_t ax = meta >> 24;
     const uint32_t f0 = ~(dpos >> (ax & 3u)) & 1u;
     const uint32_t f1 = ~(dpos >> ((ax >> 2) & 3u)) & 1u;
@@ -229,7 +229,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, co
 #pragma unroll
     for (int k = 0; k < 4; k++) pm |= hit[k] ? (1u << pos[k]) : 0u;
     if (pm == 0) {
-        cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim, base);
+        cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim);
         return;
     }
     const uint32_t rest = pm & (pm - 1u);  // entered slots after the first: pushed
@@ -310,8 +310,7 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
 template <bool ANY>
 __device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, V3 o, uint32_t dpos, V3 invd, float tmin,
                                                float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
-                                               uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp,
-                                               int base = 0) {
+                                               uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
     const uint4 *wu = reinterpret_cast<const uint4 *>(wn);
     const float4 h = wn[4 * (size_t)cur + 0];
     const uint4 c = wu[4 * (size_t)cur + 1];
@@ -360,8 +359,7 @@ __device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, 
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid, sp,
-                         base);
+    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid, sp);
     return tested;
 }
 
@@ -510,25 +508,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     int sp = 0;
     uint32_t steps = 0;  // COUNT only (ray_steps diagnostic)
     bool busy = false, occluded = false, drained = n == 0;
-    // Cooperative tail (closest hit): once the queue is drained, idle lanes take
-    // subtrees from the bottom of busy lanes' stacks (the last ones in depth-first order) and
-    // traverse them with the donor's current best as their bound; the donor merges the results in
-    // depth-first order when it and its helpers are done.
-    constexpr bool COOP = kCoop && MODE == TRACE_CLOSEST && WIDE && TIGHT;
-    __shared__ float s_best[COOP ? kBlock : 1];
-    __shared__ float4 s_res[COOP ? kBlock : 1];  // a finished helper's result: t (negated: eflag), u, v, gid
-    const uint32_t lane = __lane_id();
-    const uint32_t wbase = tid & ~63u;  // first thread of this wave in the block
-    int base = 0;          // stack bottom: entries below it were donated
-    int par = -1;          // helper: the donor lane; -1: this lane owns its ray
-    uint32_t ndon = 0;     // donations made (<= kMaxDonations)
-    uint32_t don = 0;      // their helper lanes, 6 bits each, in donation order
-    float bt = kInf;       // t of the last accepted triangle (best can be lower in a helper)
-    bool pend = false;     // own part done, waiting for the donated subtrees
-    bool fin = false;      // helper done: result in its LDS stack column, waiting for the merge
-    bool eflag = false;    // a helper accepted a triangle nearer than its leaf box's entry
     bool need_exact = false;  // trace this lane's ray with the exact BVH2 walk (end of iteration)
-    uint32_t nvis = 0;     // traversal iterations of this lane's current ray part
     // The queue [0, n) is cut into kWorkShards contiguous ranges, each with its own counter on its
     // own 128-B line: one counter word saturates at ~88 returning atomics/us chip-wide, so a
     // single shared counter capped the refill rate.  A wave starts on shard blockIdx % 8 (the
@@ -576,111 +556,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 }
             }
         }
-        if (COOP && drained && !(a.coop & AKR_COOP_OFF)) {
-            // (a) bounds: a helper may cull with its donor's current best, which is >= the best the
-            // sequential traversal would carry into the helper's subtree
-            s_best[tid] = best;
-            __builtin_amdgcn_wave_barrier();  // same-wave LDS: the reads below follow the writes
-            if (busy && par >= 0) best = fminf(best, s_best[wbase + par]);
-            // (b) merges: a waiting lane whose helpers have all finished folds their results in
-            // depth-first order (latest donation first; strict < keeps the earliest of equal t)
-            const unsigned long long F = __ballot(fin);
-            bool ready = pend;
-            for (uint32_t j = 0; j < ndon; j++) ready = ready && ((F >> ((don >> (6 * j)) & 63u)) & 1ull);
-            if (ready) {
-                for (int j = (int)ndon - 1; j >= 0; j--) {
-                    const float4 r = s_res[wbase + ((don >> (6 * j)) & 63u)];
-                    const float th = fabsf(r.x);  // hit t > tmin >= 0 (or +inf): the sign is eflag
-                    if (th < bt) {
-                        bt = th;
-                        bu = r.y;
-                        bv = r.z;
-                        bgid = fbits(r.w);
-                    }
-                    eflag = eflag || signbit(r.x);
-                }
-                pend = false;
-                ndon = 0;
-                don = 0;
-                if (par < 0) {
-                    if (eflag) need_exact = true;  // possible rounding divergence: exact re-trace
-                    else {
-                        emit_result<MODE>(a, idx, bt, bu, bv, bgid, false);
-                        if (COUNT && a.ray_steps) a.ray_steps[idx] = steps;
-                    }
-                } else {
-                    s_res[tid] = make_float4(eflag ? -bt : bt, bu, bv, bitsf(bgid));
-                    fin = true;
-                }
-            }
-            // (c) a finished helper whose donor merged this round is free again
-            const unsigned long long M = __ballot(ready);
-            if (((F >> lane) & 1ull) && par >= 0 && ((M >> par) & 1ull)) {
-                fin = false;
-                par = -1;
-            }
-            // (d) donations: busy lanes hand their bottom stack entry to idle lanes, one each
-            const bool can = busy && sp > base && ndon < (uint32_t)kMaxDonations && nvis >= (a.coop >> 8) &&
-                             (!(a.coop & AKR_COOP_HIT_ONLY) || best < kInf);
-            unsigned long long ebot = 0;
-            if (can) {
-                ebot = base < kStackLds ? s_stack[base * kBlock + tid]
-                                        : stack_ovf[(size_t)(base - kStackLds) * a.ovf_threads + gtid];
-                if (__uint_as_float((uint32_t)(ebot >> 32)) > best) base++;  // would be culled when popped
-            }
-            unsigned long long D = __ballot(can && !(__uint_as_float((uint32_t)(ebot >> 32)) > best));
-            // (a lane refilled in this same iteration, `fresh`, is not idle: its ray starts below)
-            unsigned long long I = __ballot(!busy && !fresh && !pend && !fin && !need_exact);
-            uint32_t src = lane;
-            bool take = false;
-            while (D && I) {  // wave-uniform: pair the k-th donor with the k-th idle lane
-                const uint32_t dl = (uint32_t)__builtin_ctzll(D), il = (uint32_t)__builtin_ctzll(I);
-                D &= D - 1;
-                I &= I - 1;
-                if (lane == dl) {
-                    don |= il << (6 * ndon);
-                    ndon++;
-                    base++;
-                }
-                if (lane == il) {
-                    src = dl;
-                    take = true;
-                }
-            }
-            if (__any(take)) {
-                const float hox = __shfl(o.x, (int)src), hoy = __shfl(o.y, (int)src), hoz = __shfl(o.z, (int)src);
-                const float hdx = __shfl(d.x, (int)src), hdy = __shfl(d.y, (int)src), hdz = __shfl(d.z, (int)src);
-                const float hix = __shfl(invd.x, (int)src), hiy = __shfl(invd.y, (int)src), hiz = __shfl(invd.z, (int)src);
-                const float htmin = __shfl(tmin, (int)src), htmax = __shfl(tmax, (int)src);
-                const float htmaxp = __shfl(tmaxp, (int)src), hbest = __shfl(best, (int)src);
-                const uint32_t hdpos = __shfl(dpos, (int)src);
-                const uint32_t eref = __shfl((uint32_t)ebot, (int)src), et = __shfl((uint32_t)(ebot >> 32), (int)src);
-                if (take) {
-                    o = V3{hox, hoy, hoz};
-                    d = V3{hdx, hdy, hdz};
-                    invd = V3{hix, hiy, hiz};
-                    tmin = htmin;
-                    tmax = htmax;
-                    tmaxp = htmaxp;
-                    dpos = hdpos;
-                    lean = true;
-                    best = hbest;
-                    bt = kInf;
-                    bu = bv = 0.0f;
-                    bgid = kNoHit;
-                    occluded = false;
-                    eflag = false;
-                    par = (int)src;
-                    nvis = 0;
-                    sp = 0;
-                    base = 0;
-                    leaf = AKR_CHILD_EMPTY;
-                    cur = __uint_as_float(et) > best ? AKR_CHILD_EMPTY : eref;
-                    busy = true;
-                }
-            }
-        }
-        if (!__any(busy || fresh || pend || fin || need_exact)) {
+        if (!__any(busy || fresh || need_exact)) {
             if (drained) break;
             continue;
         }
@@ -694,12 +570,11 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                     c_sleaf += busy ? 1 : 0;
                     steps += busy ? 1 : 0;
                 }
-                if (COOP) nvis++;
                 if (WIDE && busy && is_internal(cur)) {
                     int nt;
                     if (TIGHT)  // every wide-loop ray of the tight kernel is lean (others: exact lane)
                         nt = visit_wide_lean<ANY>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
-                                                  a.ovf_threads, tid, gtid, sp, base);
+                                                  a.ovf_threads, tid, gtid, sp);
                     else
                         nt = visit_wide<TIGHT, ANY>(wn, cur, o, dpos, invd, tmin, tmax, best, s_stack, stack_ovf,
                                                     a.ovf_threads, tid, gtid, sp);
@@ -721,12 +596,16 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 }
                 if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
                     leaf = cur;  // postpone the leaf and keep descending
-                    cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best, base);
+                    cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
                 }
                 // leave for the leaf phase once at most kWhileExit lanes are still searching for
-                // their first leaf (0: every lane holds a leaf or is done — classic while-while)
-                if ((uint32_t)__popcll(__ballot(busy && leaf == AKR_CHILD_EMPTY && cur != AKR_CHILD_EMPTY)) <=
-                    (uint32_t)kWhileExit)
+                // their first leaf (0: every lane holds a leaf or is done — classic while-while),
+                // but not while nobody holds a leaf yet and someone still searches: the leaf phase
+                // would have nothing to do (a wave's last rays would pay a full outer iteration per
+                // node visit)
+                const unsigned long long searching = __ballot(busy && leaf == AKR_CHILD_EMPTY && cur != AKR_CHILD_EMPTY);
+                if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+                    (searching == 0 || __ballot(busy && leaf != AKR_CHILD_EMPTY) != 0))
                     break;
             }
             // ---- 3. leaf phase
@@ -734,14 +613,13 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 uint32_t cnt;
                 const float4 *tp;  // this leaf's triangle records (3 x float4 each)
                 float4 pa, pb, pc;  // the first one, fetched together with the leaf header
-                float tl = 0.0f;    // the leaf box's entry distance (wide)
                 if (WIDE) {  // the leaf's exact box, with the current best: the BVH2 pop-time test
                     const float4 *lr = a.wide_leaves + (leaf & 0x7FFFFFFFu);
                     const float4 l0 = lr[0], l1 = lr[1];  // lo.xyz hi.x | hi.yz first count
                     pa = lr[2];
                     pb = lr[3];
                     pc = lr[4];
-                    tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
+                    const float tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
                     const bool in = !(tl < 0.0f || tl > (ANY ? tmax : best));
                     if (COUNT) c_box++;
                     cnt = in ? fbits(l1.w) : 0u;
@@ -768,11 +646,6 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                         bu = u;
                         bv = v;
                         bgid = fbits(ta.w);
-                        if (COOP) {
-                            bt = t;
-                            // exactness guard of the cooperative tail
-                            if (par >= 0 && (t < tl || (a.coop & AKR_COOP_FORCE_EXACT))) eflag = true;
-                        }
                         if (ANY) {
                             occluded = true;
                             break;
@@ -783,15 +656,8 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             }
             if (busy && ((ANY && occluded) || cur == AKR_CHILD_EMPTY)) {
                 busy = false;
-                if (COOP && ndon) {
-                    pend = true;  // merged in the cooperative step once the helpers finish
-                } else if (COOP && par >= 0) {
-                    s_res[tid] = make_float4(eflag ? -bt : bt, bu, bv, bitsf(bgid));
-                    fin = true;
-                } else {
-                    emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
-                    if (COUNT && a.ray_steps) a.ray_steps[idx] = steps;
-                }
+                emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
+                if (COUNT && a.ray_steps) a.ray_steps[idx] = steps;
             }
         }
         if (fresh) {
@@ -817,13 +683,8 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             trace_exact_lane<MODE, TIGHT>(a, idx, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid);
             if (COUNT && a.ray_steps) a.ray_steps[idx] = 0xFFFFFFFFu;  // traced outside the wide loop
             need_exact = false;
-            eflag = false;
         }
         if (fresh) {
-            bt = kInf;
-            base = 0;
-            par = -1;
-            nvis = 0;
             best = kInf;
             bu = bv = 0.0f;
             bgid = kNoHit;

@@ -75,9 +75,6 @@ def main():
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
     ap.add_argument("--lean", type=int, default=1, help="lean slot tests in the wide traversal (0: reference arithmetic)")
-    ap.add_argument("--coop", type=int, default=1, help="cooperative tail traversal (0: off)")
-    ap.add_argument("--coop-hit-only", type=int, default=0, help="tuning: donate only after a hit")
-    ap.add_argument("--coop-min-iters", type=int, default=0, help="tuning: traversal iterations before donating")
     ap.add_argument("--timed-stats", type=int, default=1,
                     help="per-kernel HIP events inside the timed region (0: probe their overhead)")
     ap.add_argument("--emulate-world", type=int, default=0,
@@ -112,12 +109,6 @@ def main():
     ctx.set_option("wide", args.wide)
     if not args.lean:
         ctx.set_option("lean", 0)
-    if args.coop != 1:
-        ctx.set_option("coop", args.coop)
-    if args.coop_hit_only:
-        ctx.set_option("coop_hit_only", 1)
-    if args.coop_min_iters:
-        ctx.set_option("coop_min_iters", args.coop_min_iters)
     log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 
