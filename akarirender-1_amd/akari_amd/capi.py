@@ -96,9 +96,6 @@ TRI_DTYPE = np.dtype([("v0", np.float32, 3), ("gid", np.uint32), ("e1", np.float
                       ("e2", np.float32, 3), ("_p1", np.uint32)])
 NODE4_DTYPE = np.dtype([("origin", np.float32, 3), ("meta", np.uint32), ("child", np.uint32, 4),
                         ("q", np.uint32, 6), ("_pad", np.uint32, 2)])
-NODE8_DTYPE = np.dtype([("origin", np.float32, 3), ("meta", np.uint32), ("child", np.uint32, 8),
-                        ("q", np.uint32, 12), ("axes", np.uint32), ("_pad", np.uint32, 7)])
-assert NODE8_DTYPE.itemsize == 128
 LEAF_DTYPE = np.dtype([("lo", np.float32, 3), ("hi", np.float32, 3), ("first", np.uint32), ("count", np.uint32)])
 assert RAY_DTYPE.itemsize == 32 and HIT_DTYPE.itemsize == 32
 assert NODE_DTYPE.itemsize == 64 and TRI_DTYPE.itemsize == 48
@@ -143,8 +140,6 @@ EXPORTS = {
     "akr_bvh_host_wide": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "akr_bvh_host_wide_nodes": (_P, [_P]),
     "akr_bvh_host_wide_leaves": (_P, [_P]),
-    "akr_bvh_host_wide8": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
-    "akr_bvh_host_wide8_nodes": (_P, [_P]),
 }
 
 _lib = None
@@ -174,8 +169,7 @@ def device_count() -> int:
 def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0,
                    n_threads=0, wide=False):
     """Run the product BVH builder on the host (no device): returns (nodes, tris, info), plus
-    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide` (True or 4), of the
-    8-wide view when wide == 8."""
+    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide`."""
     lib = load_library()
     v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
     i = np.ascontiguousarray(indices, np.int32).reshape(-1)
@@ -201,17 +195,8 @@ def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost
                 C.memmove(wn.ctypes.data, lib.akr_bvh_host_wide_nodes(h), wn.nbytes)
             if lv.nbytes:
                 C.memmove(lv.ctypes.data, lib.akr_bvh_host_wide_leaves(h), lv.nbytes)
-            if wide == 8:
-                n8, root8 = C.c_uint64(0), C.c_uint32(0)
-                if lib.akr_bvh_host_wide8(h, C.byref(n8), C.byref(root8)) != 0:
-                    raise AkrError("akr_bvh_host_wide8 failed")
-                w8 = np.empty(n8.value, NODE8_DTYPE)
-                if w8.nbytes:
-                    C.memmove(w8.ctypes.data, lib.akr_bvh_host_wide8_nodes(h), w8.nbytes)
     finally:
         lib.akr_bvh_host_free(h)
-    if wide == 8:
-        return nodes, tris, info, (w8, lv, root8.value)
     if wide:
         return nodes, tris, info, (wn, lv, root.value)
     return nodes, tris, info

@@ -24,7 +24,7 @@ constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 #define AKR_REFILL_MIN 32
 #endif
 constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entries per ray (8 B each)
-constexpr int kStackMax = 160;        // >= 7 pushes x 22 8-wide levels (BVH2 depth <= 64)
+constexpr int kStackMax = 96;         // >= 3 pushes x 32 wide levels (BVH2 depth <= 64)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
 #ifndef AKR_WHILE_EXIT

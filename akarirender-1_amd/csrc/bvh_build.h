@@ -48,18 +48,6 @@ struct Bvh4Output {
 
 void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out);
 
-// 8-wide view of the same BVH2 (akr_bvh8_node); its leaves come in the same (BVH2 depth-first)
-// order as the 4-wide view's.
-struct Bvh8Output {
-    std::vector<akr_bvh8_node> nodes;
-    std::vector<akr_bvh_leaf> leaves;
-    uint32_t root_ref = AKR_CHILD_EMPTY;
-    int max_depth = 0;
-    float max_abs = 0.0f;
-};
-
-void build_bvh8(const std::vector<akr_bvh_node> &bvh2, Bvh8Output &out);
-
 // Outward 8-bit quantization of one bound (exposed for tests): the q with fmaf(q, s, origin) on
 // the correct side of `bound`, s = 2^(e - 127).
 uint32_t quantize_lo(float bound, float origin, float s);

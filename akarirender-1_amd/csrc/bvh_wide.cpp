@@ -1,5 +1,5 @@
-// bvh_wide.cpp — collapse the BVH2 into the 4- and 8-wide, outward-quantized views the traversal
-// kernels walk (akr_bvh4_node / akr_bvh8_node / akr_bvh_leaf, akr_bvh_format.h).
+// bvh_wide.cpp — collapse the BVH2 into the 4-wide, outward-quantized view the traversal kernels
+// walk (akr_bvh4_node / akr_bvh_leaf, akr_bvh_format.h).
 //
 // Each wide node is a BVH2 node with its two children folded in, so a traversal step replaces
 // two BVH2 levels and fetches 64 B for four child boxes instead of 2 x 64 B.  Correctness does
@@ -49,22 +49,9 @@ Box child_box(const akr_bvh_node &n, int c) {
     return b;
 }
 
-// A wide node before packing: W slots (BVH2 references + exact boxes) and the split axes of the
-// W - 1 folded BVH2 nodes, in heap order (node, its children, its grandchildren ...).
-template <int W>
-struct WideSlots {
-    uint32_t ref2[W];
-    Box box[W];
-    uint32_t axis[W - 1];
-};
-
-// Collapses a BVH2 into W-wide nodes (W = 4 or 8), depth-first preorder, leaves in BVH2
-// depth-first order.  Out is Bvh4Output or Bvh8Output; pack() writes the format's node.
-template <int W, class Out, class Node>
 struct Collapser {
-    static constexpr int L = W == 4 ? 2 : 3;  // folded BVH2 levels
     const std::vector<akr_bvh_node> &in;
-    Out &out;
+    Bvh4Output &out;
 
     uint32_t leaf_ref(uint32_t ref2, const Box &b) {
         akr_bvh_leaf l;
@@ -80,31 +67,30 @@ struct Collapser {
         return AKR_CHILD_LEAF | (uint32_t)idx;
     }
 
-    // slot group [base, base + span) at `level` below the wide node's BVH2 node: a leaf (or the
-    // bottom level) takes slot `base`; an internal node records its axis and splits the group
-    void gather(WideSlots<W> &ws, uint32_t ref, const Box &b, int level, int base, int span) {
-        if (ref == AKR_CHILD_EMPTY) return;
-        if (level == L || (ref & AKR_CHILD_LEAF)) {
-            ws.ref2[base] = ref;
-            ws.box[base] = b;
-            return;
-        }
-        const akr_bvh_node &m = in[ref];
-        ws.axis[(1 << level) - 1 + base / span] = m.axis;
-        for (int g = 0; g < 2; g++) gather(ws, m.child[g], child_box(m, g), level + 1, base + g * span / 2, span / 2);
-    }
-
     // Wide node for BVH2 internal node `n2`, laid out in depth-first preorder.
     uint32_t build(uint32_t n2, int depth) {
         if (depth > out.max_depth) out.max_depth = depth;
         const uint32_t me = (uint32_t)out.nodes.size();
         out.nodes.emplace_back();
-        WideSlots<W> ws;
-        for (int s = 0; s < W; s++) ws.ref2[s] = AKR_CHILD_EMPTY;
-        for (int a = 0; a < W - 1; a++) ws.axis[a] = 0;
         const akr_bvh_node &n = in[n2];
-        ws.axis[0] = n.axis;
-        for (int c = 0; c < 2; c++) gather(ws, n.child[c], child_box(n, c), 1, c * W / 2, W / 2);
+        uint32_t slot_ref2[4] = {AKR_CHILD_EMPTY, AKR_CHILD_EMPTY, AKR_CHILD_EMPTY, AKR_CHILD_EMPTY};
+        Box slot_box[4];
+        uint32_t axis[3] = {n.axis, 0, 0};
+        for (int c = 0; c < 2; c++) {
+            const uint32_t r = n.child[c];
+            if (r == AKR_CHILD_EMPTY) continue;
+            if (r & AKR_CHILD_LEAF) {
+                slot_ref2[2 * c] = r;
+                slot_box[2 * c] = child_box(n, c);
+            } else {
+                const akr_bvh_node &m = in[r];
+                axis[1 + c] = m.axis;
+                for (int g = 0; g < 2; g++) {
+                    slot_ref2[2 * c + g] = m.child[g];
+                    slot_box[2 * c + g] = child_box(m, g);
+                }
+            }
+        }
         // quantization frame: the union of the slot boxes
         float plo[3], phi[3];
         for (int k = 0; k < 3; k++) {
@@ -112,30 +98,31 @@ struct Collapser {
             phi[k] = -INFINITY;
         }
         bool any = false;
-        for (int s = 0; s < W; s++) {
-            if (ws.ref2[s] == AKR_CHILD_EMPTY) continue;
+        for (int s = 0; s < 4; s++) {
+            if (slot_ref2[s] == AKR_CHILD_EMPTY) continue;
             any = true;
             for (int k = 0; k < 3; k++) {
-                plo[k] = std::min(plo[k], ws.box[s].lo[k]);
-                phi[k] = std::max(phi[k], ws.box[s].hi[k]);
+                plo[k] = std::min(plo[k], slot_box[s].lo[k]);
+                phi[k] = std::max(phi[k], slot_box[s].hi[k]);
             }
         }
-        float origin[3];
+        akr_bvh4_node w;
+        std::memset(&w, 0, sizeof(w));
         uint32_t ex[3] = {1, 1, 1};
         for (int k = 0; k < 3; k++) {
             if (!any) {
-                origin[k] = 0.0f;
+                w.origin[k] = 0.0f;
                 continue;
             }
             if (!std::isfinite(plo[k]) || !std::isfinite(phi[k]))
                 throw std::runtime_error("non-finite BVH bounds");
-            origin[k] = plo[k];
+            w.origin[k] = plo[k];
             const double ext = (double)phi[k] - (double)plo[k];
             int e = -126;
             if (ext > 0) {
-                int k2 = 0;
-                std::frexp(ext / 255.0, &k2);  // ext / 255 < 2^k2
-                e = std::max(-126, k2 - 1);
+                int k = 0;
+                std::frexp(ext / 255.0, &k);  // ext / 255 < 2^k
+                e = std::max(-126, k - 1);
             }
             while (e < 127 && 255.0 * std::ldexp(1.0, e) < ext) e++;
             while (e < 127 && (std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k] || !real_ge(255, pow2f(e), plo[k], phi[k]))) e++;
@@ -144,74 +131,29 @@ struct Collapser {
             out.max_abs = std::max(out.max_abs, std::max(std::fabs(plo[k]), pow2f(e)));
             ex[k] = (uint32_t)(e + 127);
         }
-        uint8_t qlo[W][3], qhi[W][3];
-        for (int s = 0; s < W; s++)
-            for (int k = 0; k < 3; k++) {
-                qlo[s][k] = qhi[s][k] = 0;
-                if (ws.ref2[s] == AKR_CHILD_EMPTY) continue;
-                const float sc = pow2f((int)ex[k] - 127);
-                qlo[s][k] = (uint8_t)quantize_lo(ws.box[s].lo[k], origin[k], sc);
-                qhi[s][k] = (uint8_t)quantize_hi(ws.box[s].hi[k], origin[k], sc);
+        w.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | (axis[0] | axis[1] << 2 | axis[2] << 4) << 24;
+        for (int s = 0; s < 4; s++) {
+            const uint32_t r = slot_ref2[s];
+            if (r == AKR_CHILD_EMPTY) {
+                w.child[s] = AKR_CHILD_EMPTY;
+                continue;
             }
-        // children (preorder: this node first, then its slots' subtrees in slot order)
-        uint32_t child[W];
-        for (int s = 0; s < W; s++) {
-            const uint32_t r = ws.ref2[s];
-            child[s] = r == AKR_CHILD_EMPTY ? AKR_CHILD_EMPTY
-                                            : ((r & AKR_CHILD_LEAF) ? leaf_ref(r, ws.box[s]) : build(r, depth + 1));
+            for (int k = 0; k < 3; k++) {
+                const float sc = pow2f((int)ex[k] - 127);
+                w.q[2 * k] |= quantize_lo(slot_box[s].lo[k], w.origin[k], sc) << (8 * s);
+                w.q[2 * k + 1] |= quantize_hi(slot_box[s].hi[k], w.origin[k], sc) << (8 * s);
+            }
         }
-        Node w;
-        std::memset(&w, 0, sizeof(w));
-        pack(w, origin, ex, ws.axis, child, qlo, qhi);
+        // children (preorder: this node first, then its slots' subtrees in slot order)
+        for (int s = 0; s < 4; s++) {
+            const uint32_t r = slot_ref2[s];
+            if (r == AKR_CHILD_EMPTY) continue;
+            w.child[s] = (r & AKR_CHILD_LEAF) ? leaf_ref(r, slot_box[s]) : build(r, depth + 1);
+        }
         out.nodes[me] = w;
         return me;
     }
-
-    static void pack(akr_bvh4_node &w, const float *origin, const uint32_t *ex, const uint32_t *axis,
-                     const uint32_t *child, const uint8_t (*qlo)[3], const uint8_t (*qhi)[3]) {
-        for (int k = 0; k < 3; k++) w.origin[k] = origin[k];
-        w.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | (axis[0] | axis[1] << 2 | axis[2] << 4) << 24;
-        for (int s = 0; s < 4; s++) {
-            w.child[s] = child[s];
-            for (int k = 0; k < 3; k++) {
-                w.q[2 * k] |= (uint32_t)qlo[s][k] << (8 * s);
-                w.q[2 * k + 1] |= (uint32_t)qhi[s][k] << (8 * s);
-            }
-        }
-    }
-
-    static void pack(akr_bvh8_node &w, const float *origin, const uint32_t *ex, const uint32_t *axis,
-                     const uint32_t *child, const uint8_t (*qlo)[3], const uint8_t (*qhi)[3]) {
-        for (int k = 0; k < 3; k++) w.origin[k] = origin[k];
-        w.meta = ex[0] | ex[1] << 8 | ex[2] << 16;
-        w.axes = 0;
-        for (int a = 0; a < 7; a++) w.axes |= axis[a] << (2 * a);
-        for (int s = 0; s < 8; s++) {
-            w.child[s] = child[s];
-            for (int k = 0; k < 3; k++) {
-                w.q[2 * (2 * k) + (s >> 2)] |= (uint32_t)qlo[s][k] << (8 * (s & 3));
-                w.q[2 * (2 * k + 1) + (s >> 2)] |= (uint32_t)qhi[s][k] << (8 * (s & 3));
-            }
-        }
-    }
 };
-
-template <int W, class Out, class Node>
-void build_wide(const std::vector<akr_bvh_node> &bvh2, Out &out) {
-    out.nodes.clear();
-    out.leaves.clear();
-    out.max_depth = 0;
-    out.max_abs = 0.0f;
-    out.root_ref = AKR_CHILD_EMPTY;
-    if (bvh2.empty()) return;
-    const akr_bvh_node &vroot = bvh2[0];  // virtual root: child 0 = the real root
-    const uint32_t r = vroot.child[0];
-    if (r == AKR_CHILD_EMPTY) return;
-    Collapser<W, Out, Node> c{bvh2, out};
-    out.nodes.reserve(bvh2.size() / (W - 1) + 1);
-    if (r & AKR_CHILD_LEAF) out.root_ref = c.leaf_ref(r, child_box(vroot, 0));
-    else out.root_ref = c.build(r, 1);
-}
 
 }  // namespace
 
@@ -236,11 +178,19 @@ uint32_t quantize_hi(float bound, float origin, float s) {
 }
 
 void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out) {
-    build_wide<4, Bvh4Output, akr_bvh4_node>(bvh2, out);
-}
-
-void build_bvh8(const std::vector<akr_bvh_node> &bvh2, Bvh8Output &out) {
-    build_wide<8, Bvh8Output, akr_bvh8_node>(bvh2, out);
+    out.nodes.clear();
+    out.leaves.clear();
+    out.max_depth = 0;
+    out.max_abs = 0.0f;
+    out.root_ref = AKR_CHILD_EMPTY;
+    if (bvh2.empty()) return;
+    const akr_bvh_node &vroot = bvh2[0];  // virtual root: child 0 = the real root
+    const uint32_t r = vroot.child[0];
+    if (r == AKR_CHILD_EMPTY) return;
+    Collapser c{bvh2, out};
+    out.nodes.reserve(bvh2.size() / 2 + 1);
+    if (r & AKR_CHILD_LEAF) out.root_ref = c.leaf_ref(r, child_box(vroot, 0));
+    else out.root_ref = c.build(r, 1);
 }
 
 }  // namespace akr

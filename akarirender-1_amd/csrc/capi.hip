@@ -153,15 +153,12 @@ struct akr_hip_ctx {
     akr_accel_info info{};
     BvhOutput bvh;
     Bvh4Output bvh4;
-    Bvh8Output bvh8;
 
     // device scene
     DBuf<akr_bvh_node> d_nodes;
     DBuf<akr_bvh4_node> d_wnodes;
     DBuf<float4> d_wleaves;          // leaf blob (see TraceArgs::wide_leaves)
     uint32_t wide_root_dev = AKR_CHILD_EMPTY;
-    DBuf<akr_bvh8_node> d_w8nodes;   // 8-wide view (same leaf blob)
-    uint32_t wide8_root_dev = AKR_CHILD_EMPTY;
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
@@ -205,7 +202,7 @@ struct akr_hip_ctx {
     bool stats = false, count = false;
     bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
     int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
-    int wide = 4;             // quantized wide view the traversal walks: 4 or 8 (0: BVH2 kernel only, for A/B)
+    bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
     bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
     DBuf<uint32_t> d_steps;
@@ -436,21 +433,17 @@ struct akr_hip_ctx {
     // One trace launch: the 4-wide kernel (which traces its rare NaN-prone rays inline with the
     // exact BVH2 walk), or the BVH2 kernel when the "wide" option is off.
     void trace_launch(int mode, bool tight, const TraceArgs &t, uint64_t n_max, hipStream_t st) {
-        launch_trace(mode, count, tight, width(tight), t, grid_for(mode, n_max), st);
+        launch_trace(mode, count, tight, wide, t, grid_for(mode, n_max), st);
     }
 
-    // the view a launch walks: the 8-wide one has only the lean (tight) slot test
-    int width(bool tight) const { return wide == 8 && !tight ? 4 : wide; }
-
-    TraceArgs trace_args(uint32_t *work, bool tight = true) {
+    TraceArgs trace_args(uint32_t *work) {
         TraceArgs t{};
-        const bool w8 = width(tight) == 8;
         t.nodes = d_nodes.p;
-        t.wide_nodes = w8 ? reinterpret_cast<const float4 *>(d_w8nodes.p) : reinterpret_cast<const float4 *>(d_wnodes.p);
+        t.wide_nodes = reinterpret_cast<const float4 *>(d_wnodes.p);
         t.wide_leaves = reinterpret_cast<const float4 *>(d_wleaves.p);
-        t.wide_root = w8 ? wide8_root_dev : wide_root_dev;
+        t.wide_root = wide_root_dev;
         // the lean slot test's slack is derived for frame origins and steps below 2^40
-        t.lean = lean && (w8 ? bvh8.max_abs : bvh4.max_abs) <= 0x1p40f ? 1u : 0u;
+        t.lean = lean && bvh4.max_abs <= 0x1p40f ? 1u : 0u;
         t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
@@ -477,7 +470,7 @@ struct akr_hip_ctx {
         require_ready();
         if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
         HIPCHK(hipMemsetAsync(d_work.p, 0, kTraceWords * sizeof(uint32_t), st));
-        TraceArgs t = trace_args(d_work.p, !exact_cull);
+        TraceArgs t = trace_args(d_work.p);
         t.rays = rays;
         t.n = (uint32_t)n;
         t.abi_hits = hits;
@@ -487,7 +480,7 @@ struct akr_hip_ctx {
             n_steps = n;
             t.ray_steps = d_steps.p;
             timed(any ? "trace_any" : "trace_closest", st,
-                  [&] { launch_trace(mode, true, !exact_cull, width(!exact_cull), t, grid_for(mode, n), st); });
+                  [&] { launch_trace(mode, true, !exact_cull, wide, t, grid_for(mode, n), st); });
         } else {
             timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, st); });
         }
@@ -576,7 +569,7 @@ struct akr_hip_ctx {
             for (int b = 0; b < nb; b++, g++) {
                 const bool odd = b & 1;
                 const int sq = (int)(g & 1);
-                TraceArgs t = trace_args(work(b, 0), tight);
+                TraceArgs t = trace_args(work(b, 0));
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
@@ -606,7 +599,7 @@ struct akr_hip_ctx {
                 HIPCHK(hipEventRecord(ev_shade[sq], ms));
                 HIPCHK(hipStreamWaitEvent(side, ev_shade[sq], 0));
                 if (b < p.max_depth) {
-                    TraceArgs ts = trace_args(work(b, 1), tight);
+                    TraceArgs ts = trace_args(work(b, 1));
                     ts.stack_ovf = d_ovf_side.p;  // concurrent with a main-stream trace
                     ts.rays = d_sray[sq].p;
                     ts.count = scount(b);
@@ -659,7 +652,7 @@ struct akr_hip_ctx {
             HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
             const RaygenArgs rg = raygen_args((uint32_t)N, L, qcount, s == 0);
             timed("raygen", ms, [&] { launch_raygen(rg, ms); });
-            TraceArgs t = trace_args(work0, tight);
+            TraceArgs t = trace_args(work0);
             t.rays = d_ray0.p;
             t.count = qcount;
             t.hits = d_hit.p;
@@ -678,7 +671,7 @@ struct akr_hip_ctx {
             timed("ao_shade", ms, [&] { launch_ao_shade(sh, (uint32_t)N, ms); });
             HIPCHK(hipEventRecord(ev_shade[ps], ms));
             HIPCHK(hipStreamWaitEvent(side, ev_shade[ps], 0));
-            TraceArgs ts = trace_args(work1, tight);
+            TraceArgs ts = trace_args(work1);
             ts.stack_ovf = d_ovf_side.p;  // concurrent with the next pass's main-stream trace
             ts.rays = d_sray[ps].p;
             ts.count = acount;
@@ -772,9 +765,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->count = value != 0;
         } else if (k == "ray_steps") {
             ctx->ray_steps = value != 0;
-        } else if (k == "wide") {  // 0: BVH2 kernel; 1 or 4: 4-wide view; 8: 8-wide view
-            if (value != 0 && value != 1 && value != 4 && value != 8) throw std::runtime_error("wide must be 0, 1, 4 or 8");
-            ctx->wide = value == 1 ? 4 : (int)value;
+        } else if (k == "wide") {
+            ctx->wide = value != 0;
         } else if (k == "lean") {
             ctx->lean = value != 0;
         } else if (k == "rays_per_lane") {
@@ -872,9 +864,6 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         else throw std::runtime_error("unknown builder");
         auto &b = ctx->bvh;
         build_bvh4(b.nodes, ctx->bvh4);
-        build_bvh8(b.nodes, ctx->bvh8);
-        if (ctx->bvh8.leaves.size() != ctx->bvh4.leaves.size())
-            throw std::runtime_error("wide views disagree on the leaves");
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
         // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
         // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the
@@ -906,12 +895,6 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         for (auto &n : wn)
             for (auto &c : n.child) c = remap(c);
         ctx->wide_root_dev = remap(ctx->bvh4.root_ref);
-        std::vector<akr_bvh8_node> wn8 = ctx->bvh8.nodes;
-        for (auto &n : wn8)
-            for (auto &c : n.child) c = remap(c);
-        ctx->wide8_root_dev = remap(ctx->bvh8.root_ref);
-        ctx->d_w8nodes.reserve(1);
-        ctx->d_w8nodes.upload(wn8.data(), wn8.size(), ctx->stream);
         ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
         ctx->d_wleaves.reserve(1);
         ctx->d_wnodes.upload(wn.data(), wn.size(), ctx->stream);
@@ -1079,8 +1062,6 @@ struct akr_bvh_host {
     BvhOutput out;
     Bvh4Output wide;
     bool wide_built = false;
-    Bvh8Output wide8;
-    bool wide8_built = false;
 };
 
 int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t *indices, uint64_t n_triangles,
@@ -1134,22 +1115,6 @@ int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, ui
 }
 const void *akr_bvh_host_wide_nodes(const akr_bvh_host *h) { return h ? h->wide.nodes.data() : nullptr; }
 const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h) { return h ? h->wide.leaves.data() : nullptr; }
-
-int akr_bvh_host_wide8(akr_bvh_host *h, uint64_t *n_nodes, uint32_t *root_ref) {
-    if (!h) return -1;
-    try {
-        if (!h->wide8_built) {
-            build_bvh8(h->out.nodes, h->wide8);
-            h->wide8_built = true;
-        }
-        if (n_nodes) *n_nodes = h->wide8.nodes.size();
-        if (root_ref) *root_ref = h->wide8.root_ref;
-        return 0;
-    } catch (...) {
-        return -1;
-    }
-}
-const void *akr_bvh_host_wide8_nodes(const akr_bvh_host *h) { return h ? h->wide8.nodes.data() : nullptr; }
 
 int akr_hip_ray_steps(akr_hip_ctx *ctx, uint32_t *out, uint64_t n) {
     return guard(ctx, [&] {

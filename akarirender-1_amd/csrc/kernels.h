@@ -7,8 +7,7 @@ namespace akr {
 enum : int { TRACE_CLOSEST = 0, TRACE_ANY = 1, TRACE_SHADOW = 2 };
 
 // tight = standard slab test (default); !tight = the reference's intersectAABB, bit for bit
-// wide: 0 = BVH2 kernel, 4 / 8 = the 4- / 8-wide view (8 needs tight)
-void launch_trace(int mode, bool count, bool tight, int wide, const TraceArgs &a, uint32_t grid, hipStream_t st);
+void launch_trace(int mode, bool count, bool tight, bool wide, const TraceArgs &a, uint32_t grid, hipStream_t st);
 int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);

@@ -14,8 +14,6 @@
 #include "akr_math.h"
 #include "kernels.h"
 
-#include <stdexcept>
-
 namespace akr {
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -211,60 +209,42 @@ __device__ __forceinline__ float ubyte(uint32_t w, int k) {  // v_cvt_f32_ubyte{
 
 // Continue with the first entered slot of a wide node in the BVH2 depth-first order and push the
 // other entered slots behind it, each with its entry distance; pop when no slot is entered.
-// `dpos` holds the ray's direction signs: bit a = (d[a] > 0); `axes` the split axes of the folded
-// BVH2 nodes in heap order (2 bits each: the node, its children, its grandchildren).  The order is
-// a permutation of the slots by flip bits f(i) = !(d[axis_i] > 0) (near = left iff d[axis] > 0 at
-// each folded node): position(slot k) = k ^ (f(node) << (L-1) | f(child k>>(L-1)) << (L-2) | ...).
-// Entered slots are ranked by position without moving any data: the first becomes `cur`, each
-// other one is written straight to its stack entry sp + (number of entered slots at later
-// positions), so the earliest is popped first.
-template <int W, bool ANY>
-__device__ __forceinline__ void wide_order_push(uint32_t axes, uint32_t dpos, const float (&t)[W], const bool (&hit)[W],
-                                                const uint32_t (&ref)[W], uint32_t &cur, float lim, lds_u64 *s_stack,
+// `dpos` holds the ray's direction signs: bit a = (d[a] > 0).  The order is a permutation of the
+// slots by three flip bits (near = left iff d[axis] > 0 at each of the three folded BVH2 nodes):
+// position(slot k) = k ^ (f0 << 1 | f_{1 + k/2}).  Entered slots are ranked by position without
+// moving any data: the first becomes `cur`, each other one is written straight to its stack entry
+// sp + (number of entered slots at later positions), so the earliest is popped first.
+template <bool ANY>
+__device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, const float (&t)[4], const bool (&hit)[4],
+                                                const uint32_t (&ref)[4], uint32_t &cur, float lim, lds_u64 *s_stack,
                                                 glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
                                                 int &sp) {
-    auto flip = [&](int i) { return ~(dpos >> ((axes >> (2 * i)) & 3u)) & 1u; };
-    uint32_t pos[W];
-    if (W == 4) {
-        const uint32_t f0 = flip(0);
-        const uint32_t m01 = (f0 << 1) | flip(1), m23 = (f0 << 1) | flip(2);
-        pos[0] = m01;
-        pos[1] = 1u ^ m01;
-        pos[2] = 2u ^ m23;
-        pos[3] = 3u ^ m23;
-    } else {
-        const uint32_t f0 = flip(0) << 2;
-        const uint32_t c0 = f0 | (flip(1) << 1), c1 = f0 | (flip(2) << 1);
-        const uint32_t m[4] = {c0 | flip(3), c0 | flip(4), c1 | flip(5), c1 | flip(6)};
-#pragma unroll
-        for (int k = 0; k < W; k++) pos[k % W] = (uint32_t)k ^ m[(k % W) >> 1];
-    }
+    const uint32_t ax = meta >> 24;
+    const uint32_t f0 = ~(dpos >> (ax & 3u)) & 1u;
+    const uint32_t f1 = ~(dpos >> ((ax >> 2) & 3u)) & 1u;
+    const uint32_t f2 = ~(dpos >> ((ax >> 4) & 3u)) & 1u;
+    const uint32_t m01 = (f0 << 1) | f1, m23 = (f0 << 1) | f2;
+    const uint32_t pos[4] = {m01, 1u ^ m01, 2u ^ m23, 3u ^ m23};
     uint32_t pm = 0;  // entered slots, by position
 #pragma unroll
-    for (int k = 0; k < W; k++) pm |= hit[k] ? (1u << pos[k]) : 0u;
+    for (int k = 0; k < 4; k++) pm |= hit[k] ? (1u << pos[k]) : 0u;
     if (pm == 0) {
         cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim);
         return;
     }
     const uint32_t rest = pm & (pm - 1u);  // entered slots after the first: pushed
-    if (W == 4 && sp + 4 <= kStackLds) {
+    if (sp + 4 <= kStackLds) {
         // all in LDS: four unconditional writes, no exec-mask branches; a slot that is not pushed
         // writes entry sp + 3, which lies above the new top (sp grows by at most 3) and is dead
 #pragma unroll
-        for (int k = 0; k < W; k++) {
+        for (int k = 0; k < 4; k++) {
             const bool push = (rest >> pos[k]) & 1u;
             const int e = sp + (push ? (int)__popc(rest >> (pos[k] + 1u)) : 3);
             s_stack[e * kBlock + tid] = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
         }
-    } else if (W == 8 && sp + (int)__popc(rest) <= kStackLds) {
-#pragma unroll
-        for (int k = 0; k < W; k++)
-            if ((rest >> pos[k]) & 1u)
-                s_stack[(sp + (int)__popc(rest >> (pos[k] + 1u))) * kBlock + tid] =
-                    (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
     } else {
 #pragma unroll
-        for (int k = 0; k < W; k++) {
+        for (int k = 0; k < 4; k++) {
             if ((rest >> pos[k]) & 1u) {
                 const int e = sp + (int)__popc(rest >> (pos[k] + 1u));
                 const unsigned long long v = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
@@ -278,7 +258,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t axes, uint32_t dpos, co
     const uint32_t first = pm ^ rest;
     uint32_t c = AKR_CHILD_EMPTY;
 #pragma unroll
-    for (int k = 0; k < W; k++) c = ((first >> pos[k]) & 1u) ? ref[k] : c;
+    for (int k = 0; k < 4; k++) c = ((first >> pos[k]) & 1u) ? ref[k] : c;
     cur = c;
 }
 
@@ -310,7 +290,7 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    wide_order_push<4, ANY>(meta >> 24, dpos, t, hit, ref, cur, lim, s_stack, ovf, ovf_threads, tid, gtid, sp);
+    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, lim, s_stack, ovf, ovf_threads, tid, gtid, sp);
     return tested;
 }
 
@@ -379,59 +359,7 @@ __device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, 
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    wide_order_push<4, ANY>(meta >> 24, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid,
-                            gtid, sp);
-    return tested;
-}
-
-// visit_wide_lean for the 8-wide view (akr_bvh8_node, 128 B: seven 16-B loads per visit).
-template <bool ANY>
-__device__ __forceinline__ int visit_wide8_lean(const float4 *wn, uint32_t &cur, V3 o, uint32_t dpos, V3 invd,
-                                                float tmin, float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
-                                                uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
-    const uint4 *wu = reinterpret_cast<const uint4 *>(wn);
-    const size_t nb = 8 * (size_t)cur;
-    const float4 h = wn[nb + 0];
-    const uint4 ca = wu[nb + 1], cb = wu[nb + 2];
-    const uint4 qx = wu[nb + 3], qy = wu[nb + 4], qz = wu[nb + 5];
-    const uint32_t axes = wu[nb + 6].x;
-    const uint32_t meta = __float_as_uint(h.w);
-    constexpr float kRel = 0x1p-21f;   // 8u
-    constexpr float kAbs = 0x1p-120f;  // covers an underflowing sc
-    const float scx = __uint_as_float((meta & 0xFFu) << 23) * invd.x;
-    const float scy = __uint_as_float(((meta >> 8) & 0xFFu) << 23) * invd.y;
-    const float scz = __uint_as_float(((meta >> 16) & 0xFFu) << 23) * invd.z;
-    const float oqx = (h.x - o.x) * invd.x, oqy = (h.y - o.y) * invd.y, oqz = (h.z - o.z) * invd.z;
-    const float ex = __builtin_fmaf(__builtin_fmaf(255.0f, fabsf(scx), fabsf(oqx)), kRel, kAbs);
-    const float ey = __builtin_fmaf(__builtin_fmaf(255.0f, fabsf(scy), fabsf(oqy)), kRel, kAbs);
-    const float ez = __builtin_fmaf(__builtin_fmaf(255.0f, fabsf(scz), fabsf(oqz)), kRel, kAbs);
-    const float nox = oqx - ex, noy = oqy - ey, noz = oqz - ez;  // entry side
-    const float fox = oqx + ex, foy = oqy + ey, foz = oqz + ez;  // exit side
-    const bool px = invd.x > 0.0f, py = invd.y > 0.0f, pz = invd.z > 0.0f;
-    // words: (lo slots 0-3, lo slots 4-7, hi slots 0-3, hi slots 4-7) per axis
-    const uint32_t qn[3][2] = {{px ? qx.x : qx.z, px ? qx.y : qx.w}, {py ? qy.x : qy.z, py ? qy.y : qy.w},
-                               {pz ? qz.x : qz.z, pz ? qz.y : qz.w}};
-    const uint32_t qf[3][2] = {{px ? qx.z : qx.x, px ? qx.w : qx.y}, {py ? qy.z : qy.x, py ? qy.w : qy.y},
-                               {pz ? qz.z : qz.x, pz ? qz.w : qz.y}};
-    const float lim = ANY ? tmaxp : fminf(best, tmaxp);
-    float t[8];
-    bool hit[8];
-    const uint32_t ref[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const int w = k >> 2, by = k & 3;
-        const float nx = __builtin_fmaf(ubyte(qn[0][w], by), scx, nox), fx = __builtin_fmaf(ubyte(qf[0][w], by), scx, fox);
-        const float ny = __builtin_fmaf(ubyte(qn[1][w], by), scy, noy), fy = __builtin_fmaf(ubyte(qf[1][w], by), scy, foy);
-        const float nz = __builtin_fmaf(ubyte(qn[2][w], by), scz, noz), fz = __builtin_fmaf(ubyte(qf[2][w], by), scz, foz);
-        const float tk = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
-        const float m1 = fminf(fminf(fx, fy), fminf(fz, lim));
-        t[k] = tk;
-        hit[k] = ref[k] != AKR_CHILD_EMPTY && tk <= m1;
-    }
-    int tested = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) tested += ref[k] != AKR_CHILD_EMPTY;
-    wide_order_push<8, ANY>(axes, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid, sp);
+    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid, sp);
     return tested;
 }
 
@@ -555,7 +483,7 @@ __device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t id
 #define AKR_TRACE_WAVES 5
 #endif
 #define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
-template <int MODE, bool COUNT, bool TIGHT, int WIDE>  // WIDE: 0 (BVH2), 4 or 8 (wide views)
+template <int MODE, bool COUNT, bool TIGHT, bool WIDE>
 __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
     __shared__ unsigned long long s_stack_mem[kStackLds * kBlock];
@@ -644,10 +572,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 }
                 if (WIDE && busy && is_internal(cur)) {
                     int nt;
-                    if (WIDE == 8)  // tight only (the exact cull runs the 4-wide kernel)
-                        nt = visit_wide8_lean<ANY>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
-                                                   a.ovf_threads, tid, gtid, sp);
-                    else if (TIGHT)  // every wide-loop ray of the tight kernel is lean (others: exact lane)
+                    if (TIGHT)  // every wide-loop ray of the tight kernel is lean (others: exact lane)
                         nt = visit_wide_lean<ANY>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
                                                   a.ovf_threads, tid, gtid, sp);
                     else
@@ -767,7 +692,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
             sp = 0;
             leaf = AKR_CHILD_EMPTY;
             if (COUNT) { c_rays++; c_box++; steps = 0; }
-            const float tr = box_test<TIGHT, (WIDE != 0)>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+            const float tr = box_test<TIGHT, WIDE>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
             cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
             busy = true;
         }
@@ -1103,13 +1028,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint
 // ------------------------------------------------------------------------------------ launch
 static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
-template <int MODE, int WIDE>
+template <int MODE, bool WIDE>
 static void launch_trace_mode(bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
-    if constexpr (WIDE == 8) {  // tight only
-        if (count) hipLaunchKernelGGL((k_trace<MODE, true, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_trace<MODE, false, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
-        return;
-    }
     if (count) {
         if (tight) hipLaunchKernelGGL((k_trace<MODE, true, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
         else hipLaunchKernelGGL((k_trace<MODE, true, false, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -1119,23 +1039,16 @@ static void launch_trace_mode(bool count, bool tight, const TraceArgs &a, uint32
     }
 }
 
-template <int WIDE>
-static void launch_trace_width(int mode, bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
-    if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, WIDE>(count, tight, a, grid, st);
-    else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, WIDE>(count, tight, a, grid, st);
-    else launch_trace_mode<TRACE_SHADOW, WIDE>(count, tight, a, grid, st);
-}
-
-void launch_trace(int mode, bool count, bool tight, int wide, const TraceArgs &a, uint32_t grid, hipStream_t st) {
+void launch_trace(int mode, bool count, bool tight, bool wide, const TraceArgs &a, uint32_t grid, hipStream_t st) {
     if (grid == 0) return;
-    if (wide == 8) {
-        // the 8-wide kernel has only the lean (tight) slot test; the exact cull takes the 4-wide one
-        if (tight) launch_trace_width<8>(mode, count, tight, a, grid, st);
-        else throw std::runtime_error("the 8-wide view needs the tight cull");
-    } else if (wide) {
-        launch_trace_width<4>(mode, count, tight, a, grid, st);
+    if (wide) {
+        if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, true>(count, tight, a, grid, st);
+        else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, true>(count, tight, a, grid, st);
+        else launch_trace_mode<TRACE_SHADOW, true>(count, tight, a, grid, st);
     } else {
-        launch_trace_width<0>(mode, count, tight, a, grid, st);
+        if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, false>(count, tight, a, grid, st);
+        else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, false>(count, tight, a, grid, st);
+        else launch_trace_mode<TRACE_SHADOW, false>(count, tight, a, grid, st);
     }
 }
 
@@ -1143,11 +1056,11 @@ int trace_blocks_per_cu(int mode) {
     int nb = 0;
     hipError_t e;
     if (mode == TRACE_CLOSEST)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true, 4>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true, true>, kBlock, 0);
     else if (mode == TRACE_ANY)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true, 4>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true, true>, kBlock, 0);
     else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true, 4>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true, true>, kBlock, 0);
     if (e != hipSuccess || nb <= 0) nb = 1;
     return nb;
 }

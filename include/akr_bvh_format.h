@@ -64,21 +64,6 @@ typedef struct akr_bvh4_node {
     uint32_t _pad[2];
 } akr_bvh4_node;
 
-/* 8-wide view (three BVH2 levels folded into one node): slot k = b2 b1 b0 in binary is
- * reached from the BVH2 node by child b2, then b1, then b0 (a leaf met earlier takes the first slot
- * of its group, the others stay EMPTY).  axes holds the split axes of the seven folded BVH2 nodes,
- * 2 bits each: the node, its children 0 and 1, its grandchildren 00, 01, 10, 11.  Bound b (lo_x,
- * hi_x, lo_y, hi_y, lo_z, hi_z) of slot k is byte (k & 3) of q[2 * b + (k >> 2)]; same outward
- * quantization and exactness argument as the 4-wide view.  128 bytes: one L2 line. */
-typedef struct akr_bvh8_node {
-    float origin[3];
-    uint32_t meta;     /* ex | ey << 8 | ez << 16 */
-    uint32_t child[8]; /* wide node index, AKR_CHILD_LEAF | leaf index, or AKR_CHILD_EMPTY */
-    uint32_t q[12];
-    uint32_t axes;
-    uint32_t _pad[7];
-} akr_bvh8_node;
-
 typedef struct akr_bvh_leaf {
     float lo[3];
     float hi[3];

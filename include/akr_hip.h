@@ -240,10 +240,6 @@ void akr_bvh_host_free(akr_bvh_host *h);
 int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, uint32_t *root_ref);
 const void *akr_bvh_host_wide_nodes(const akr_bvh_host *h);
 const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h);
-/* The 8-wide view (akr_bvh8_node) of the handle's BVH2, built on first call; its leaves are the
- * 4-wide view's (same records, same order).  Pointer valid until akr_bvh_host_free. */
-int akr_bvh_host_wide8(akr_bvh_host *h, uint64_t *n_nodes, uint32_t *root_ref);
-const void *akr_bvh_host_wide8_nodes(const akr_bvh_host *h);
 
 int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n);
 int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);

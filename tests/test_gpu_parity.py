@@ -340,24 +340,3 @@ def test_trace_small_batches_and_grazing(hip_ctx_factory):
         rays["d"] = d.astype(np.float32)
         _check_trace(ctx, orc, cs, rays, False)
         _check_trace(ctx, orc, cs, rays, True)
-
-
-@pytest.mark.parametrize("mk", ["cornell", "soup", "soup_lbvh"])
-def test_wide8_trace_and_render_bit_exact(hip_ctx_factory, mk):
-    """The 8-wide view (option wide = 8): traces (closest, any, edge rays, a one-ray launch) and
-    renders bit-exact against the oracle, as for the 4-wide view."""
-    with hip_ctx_factory(0) as ctx:
-        kw = {"builder": capi.BUILDER_LBVH} if mk == "soup_lbvh" else {}
-        sc = cornell((48, 48)) if mk == "cornell" else small_soup(100_000)
-        cs, orc = _setup(ctx, sc, **kw)
-        ctx.set_option("wide", 8)
-        rays = random_rays(1 << 16, 41, -0.9, 0.9) if mk == "cornell" else random_rays(1 << 16, 41, -1.2, 1.2)
-        if mk == "cornell":
-            rays["o"][:, 1] += 1.0
-        for any_hit in (False, True):
-            _check_trace(ctx, orc, cs, rays, any_hit)
-            _check_trace(ctx, orc, cs, edge_rays((0.0, 1.0, 0.0) if mk == "cornell" else (0.0, 0.0, 0.0)), any_hit)
-        _check_trace(ctx, orc, cs, rays[:1], False)
-        _check_trace(ctx, orc, cs, rays, False, exact=True)  # the exact cull runs the 4-wide kernel
-        W, H = (48, 48) if mk == "cornell" else (96, 54)
-        _check_render(ctx, orc, 3, 5, [(0, 0, W, H)], W, H)

@@ -2,7 +2,6 @@
 builder-independence, scene language, soup generator (no GPU needed)."""
 import ctypes as C
 import re
-from fractions import Fraction
 
 import numpy as np
 import pytest
@@ -124,62 +123,6 @@ def test_wide_view_invariants(leaf):
             for i, path in walk:
                 for lo, hi in path:
                     assert np.all(lo <= lv[i]["lo"]) and np.all(hi >= lv[i]["hi"])
-
-
-def _wide8_walk(wide, signs):
-    """Depth-first walk of the 8-wide view with the kernel's slot order: position(slot k) =
-    k ^ (f(node) << 2 | f(child k >> 2) << 1 | f(grandchild k >> 1)), f(i) = !(d[axis_i] > 0)."""
-    wn, lv, root = wide
-    out = []
-
-    def slot_box(nd, k):
-        ex = [(int(nd["meta"]) >> (8 * a)) & 0xFF for a in range(3)]
-        s = [Fraction(2) ** (e - 127) for e in ex]
-        lo, hi = [], []
-        for a in range(3):
-            ql = (int(nd["q"][2 * (2 * a) + (k >> 2)]) >> (8 * (k & 3))) & 0xFF
-            qh = (int(nd["q"][2 * (2 * a + 1) + (k >> 2)]) >> (8 * (k & 3))) & 0xFF
-            lo.append(Fraction(float(nd["origin"][a])) + ql * s[a])
-            hi.append(Fraction(float(nd["origin"][a])) + qh * s[a])
-        return lo, hi
-
-    def visit(ref, path):
-        if ref == 0xFFFFFFFF:
-            return
-        if ref & 0x80000000:
-            out.append((ref & 0x7FFFFFFF, path))
-            return
-        nd = wn[ref]
-        ax = [(int(nd["axes"]) >> (2 * i)) & 3 for i in range(7)]
-        f = [0 if signs[a] else 1 for a in ax]
-        pos = [k ^ (f[0] << 2 | f[1 + (k >> 2)] << 1 | f[3 + (k >> 1)]) for k in range(8)]
-        for k in sorted(range(8), key=lambda k: pos[k]):
-            visit(int(nd["child"][k]), path + [(nd, k)] if len(out) < 400 else path)
-
-    visit(root, [])
-    return out, slot_box
-
-
-@pytest.mark.parametrize("leaf", [1, 4])
-def test_wide8_view_invariants(leaf):
-    """The 8-wide view: same leaf records as the 4-wide view, leaves reached in the BVH2
-    depth-first order for every direction octant, and each leaf's exact box inside every slot box
-    on its path in REAL arithmetic (what the lean slot test's slack assumes)."""
-    cs = scene.compile_scene(small_soup(4_000))
-    _, _, _, w4 = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, wide=True)
-    nodes, _, _, w8 = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, wide=8)
-    assert np.array_equal(w8[1], w4[1])
-    for octant in range(8):
-        signs = tuple(bool(octant >> a & 1) for a in range(3))
-        walk, slot_box = _wide8_walk(w8, signs)
-        lv = w8[1]
-        assert [(int(lv[i]["first"]), int(lv[i]["count"])) for i, _ in walk] == _bvh2_leaf_order(nodes, signs)
-        if octant == 0:
-            for i, path in walk[:400]:
-                for nd, k in path:
-                    lo, hi = slot_box(nd, k)
-                    for a in range(3):
-                        assert lo[a] <= Fraction(float(lv[i]["lo"][a])) and hi[a] >= Fraction(float(lv[i]["hi"][a]))
 
 
 @pytest.mark.parametrize("mk", ["cornell", "soup"])
