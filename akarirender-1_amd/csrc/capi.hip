@@ -202,6 +202,7 @@ struct akr_hip_ctx {
     bool stats = false, count = false;
     bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
     int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
+    int shadow_grid_pct = 100;  // persistent shadow-trace grid as a percentage of the resident maximum
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
     bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
@@ -406,7 +407,9 @@ struct akr_hip_ctx {
     uint32_t grid_for(int mode, uint64_t n) const {
         const uint64_t per_block = (uint64_t)kBlock * (uint64_t)rays_per_lane;
         uint64_t need = (n + per_block - 1) / per_block;
-        return (uint32_t)std::min<uint64_t>(need, trace_grid[mode]);
+        uint64_t cap = trace_grid[mode];
+        if (mode == TRACE_SHADOW) cap = std::max<uint64_t>(1, cap * (uint64_t)shadow_grid_pct / 100);
+        return (uint32_t)std::min<uint64_t>(need, cap);
     }
 
     void ensure_capacity(size_t n) {
@@ -769,6 +772,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->wide = value != 0;
         } else if (k == "lean") {
             ctx->lean = value != 0;
+        } else if (k == "shadow_grid_pct") {
+            if (value < 1 || value > 100) throw std::runtime_error("shadow_grid_pct must be in [1, 100]");
+            ctx->shadow_grid_pct = (int)value;
         } else if (k == "rays_per_lane") {
             if (value < 1 || value > 64) throw std::runtime_error("rays_per_lane must be in [1, 64]");
             ctx->rays_per_lane = (int)value;

@@ -97,9 +97,10 @@ __device__ __forceinline__ uint32_t lane_prefix(unsigned long long m) {
 // word sustains only ~88 returning atomics/us chip-wide (MI355X_MICROARCH.md, dequeue), so one
 // atomic per WAVE made the shade kernel atomic-bound; per workgroup it is 4x fewer.
 // Must be reached by every thread of the block.
+template <int BS = kBlock>
 __device__ __forceinline__ void block_append2(bool want_a, uint32_t *ctr_a, uint32_t &pos_a, bool want_b,
                                               uint32_t *ctr_b, uint32_t &pos_b) {
-    constexpr int kWaves = kBlock / 64;
+    constexpr int kWaves = BS / 64;
     __shared__ uint32_t s_cnt[2][kWaves];
     __shared__ uint32_t s_base[2];
     const unsigned long long ma = __ballot(want_a), mb = __ballot(want_b);
@@ -109,7 +110,7 @@ __device__ __forceinline__ void block_append2(bool want_a, uint32_t *ctr_a, uint
         s_cnt[1][w] = (uint32_t)__popcll(mb);
     }
     __syncthreads();
-    if (threadIdx.x == 0 || threadIdx.x == 64 % kBlock) {
+    if (threadIdx.x == 0 || threadIdx.x == 64 % BS) {
         const int q = threadIdx.x == 0 ? 0 : 1;
         uint32_t tot = 0;
         for (int k = 0; k < kWaves; k++) tot += s_cnt[q][k];
@@ -784,10 +785,14 @@ __device__ __forceinline__ V3 ld3(const float *p) { return v3(p[0], p[1], p[2]);
 
 // One bounce of GenericPathTracer::run_megakernel for every queued hit (pathtracer.h:137-162):
 // on_surface_scatter (:96-132) then compute_direct_lighting(select_light) (:65-91).
-__global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+#ifndef AKR_SHADE_BLOCK
+#define AKR_SHADE_BLOCK 256
+#endif
+constexpr int kShadeBlock = AKR_SHADE_BLOCK;  // threads per shade workgroup (one queue atomic each)
+__global__ __launch_bounds__(kShadeBlock) void k_shade(ShadeArgs a) {
+    const uint32_t i = blockIdx.x * kShadeBlock + threadIdx.x;
     const uint32_t n = *a.count_in;
-    if (blockIdx.x * kBlock >= n) return;  // whole workgroup past the queue (uniform: before any barrier)
+    if (blockIdx.x * kShadeBlock >= n) return;  // whole workgroup past the queue (uniform: before any barrier)
     bool want_ext = false, want_sh = false;
     float4 e0 = {}, e1 = {}, st_out = {}, s0 = {}, s1 = {}, sc = {};
     uint32_t slot = 0;
@@ -927,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(ShadeArgs a) {
         if (!want_ext) a.seed[slot] = seed;
     }
     uint32_t pos, spos;
-    block_append2(want_ext, a.count_out, pos, want_sh, a.shadow_count, spos);
+    block_append2<kShadeBlock>(want_ext, a.count_out, pos, want_sh, a.shadow_count, spos);
     if (want_ext) {
         a.ray_out[2 * (size_t)pos] = e0;
         a.ray_out[2 * (size_t)pos + 1] = e1;
@@ -1071,7 +1076,7 @@ void launch_raygen(const RaygenArgs &a, hipStream_t st) {
 }
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
-    hipLaunchKernelGGL(k_shade, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL(k_shade, dim3((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock)), dim3(kShadeBlock), 0, st, a);
 }
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;

@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
     ap.add_argument("--lean", type=int, default=1, help="lean slot tests in the wide traversal (0: reference arithmetic)")
+    ap.add_argument("--shadow-grid-pct", type=int, default=100, help="tuning: shadow-trace grid, %% of resident max")
     ap.add_argument("--timed-stats", type=int, default=1,
                     help="per-kernel HIP events inside the timed region (0: probe their overhead)")
     ap.add_argument("--emulate-world", type=int, default=0,
@@ -109,6 +110,8 @@ def main():
     ctx.set_option("wide", args.wide)
     if not args.lean:
         ctx.set_option("lean", 0)
+    if args.shadow_grid_pct != 100:
+        ctx.set_option("shadow_grid_pct", args.shadow_grid_pct)
     log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 
