@@ -189,7 +189,7 @@ struct akr_hip_ctx {
     // runs shadow traces and splat, so the last shadow trace and splat of sample pass s overlap
     // raygen and the first closest-hit trace of pass s + 1.
     hipStream_t main_st = nullptr, side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_shade[2] = {nullptr, nullptr},
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join_main = nullptr, ev_shade[2] = {nullptr, nullptr},
                ev_shadow[2] = {nullptr, nullptr}, ev_splat[2] = {nullptr, nullptr};
     DBuf<uint2> d_ovf, d_ovf_side;  // traversal stack overflow: main-stream and side-stream traces
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
@@ -227,7 +227,7 @@ struct akr_hip_ctx {
         for (auto e : pool) (void)hipEventDestroy(e);
         if (side) (void)hipStreamSynchronize(side);
         if (main_st) (void)hipStreamSynchronize(main_st);
-        for (hipEvent_t e : {ev_fork, ev_join, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1]})
+        for (hipEvent_t e : {ev_fork, ev_join, ev_join_main, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1]})
             if (e) (void)hipEventDestroy(e);
         if (main_st) (void)hipStreamDestroy(main_st);
         if (side) (void)hipStreamDestroy(side);
@@ -400,7 +400,7 @@ struct akr_hip_ctx {
         HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPCHK(hipStreamCreateWithPriority(&main_st, hipStreamNonBlocking, greatest));
         HIPCHK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, least));
-        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1]})
+        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_join_main, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
 
@@ -519,10 +519,12 @@ struct akr_hip_ctx {
 
     // the caller's stream sees every pass of both internal streams complete
     void join_streams(hipStream_t st) {
+        // one event per internal stream: re-recording a single event before the caller's stream
+        // has consumed the first wait must never be able to drop the side stream from the join
         HIPCHK(hipEventRecord(ev_join, side));
+        HIPCHK(hipEventRecord(ev_join_main, main_st));
         HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
-        HIPCHK(hipEventRecord(ev_join, main_st));
-        HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
+        HIPCHK(hipStreamWaitEvent(st, ev_join_main, 0));
         HIPCHK(hipGetLastError());
     }
 
