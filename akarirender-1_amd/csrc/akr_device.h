@@ -27,10 +27,18 @@ constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entrie
 constexpr int kStackMax = 96;         // >= 3 pushes x 32 wide levels (BVH2 depth <= 64)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
+#ifndef AKR_REFILL_MIN_ANY
+#define AKR_REFILL_MIN_ANY AKR_REFILL_MIN
+#endif
+constexpr int kRefillMinAny = AKR_REFILL_MIN_ANY;  // the same for occlusion (any-hit / shadow) traces
+#ifndef AKR_WHILE_EXIT_ANY
+#define AKR_WHILE_EXIT_ANY AKR_WHILE_EXIT
+#endif
 #ifndef AKR_WHILE_EXIT
 #define AKR_WHILE_EXIT 16
 #endif
 constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
+constexpr int kWhileExitAny = AKR_WHILE_EXIT_ANY;  // the same for occlusion traces
 #ifndef AKR_WORK_SHARDS
 #define AKR_WORK_SHARDS 8
 #endif

@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
         if (!drained) {
             const unsigned long long idle = __ballot(!busy);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= (uint32_t)kRefillMin || nidle == (uint32_t)__popcll(__ballot(1))) {
+            if (nidle >= (uint32_t)(ANY ? kRefillMinAny : kRefillMin) || nidle == (uint32_t)__popcll(__ballot(1))) {
                 const int leader = __ffsll((long long)idle) - 1;
                 uint32_t base = 0;
                 if ((int)__lane_id() == leader) base = atomicAdd(a.work + shard * kWorkStride, nidle);
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
                 // would have nothing to do (a wave's last rays would pay a full outer iteration per
                 // node visit)
                 const unsigned long long searching = __ballot(busy && leaf == AKR_CHILD_EMPTY && cur != AKR_CHILD_EMPTY);
-                if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+                if ((uint32_t)__popcll(searching) <= (uint32_t)(ANY ? kWhileExitAny : kWhileExit) &&
                     (searching == 0 || __ballot(busy && leaf != AKR_CHILD_EMPTY) != 0))
                     break;
             }
