@@ -130,6 +130,7 @@ EXPORTS = {
     "akr_hip_kernel_stats": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "akr_hip_trace_counts": (C.c_int, [_P, C.POINTER(TraceCounts)]),
     "akr_hip_reset_stats": (C.c_int, [_P]),
+    "akr_hip_render_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "akr_hip_synchronize": (C.c_int, [_P]),
     "akr_bvh_host_build": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.POINTER(BuildParams), C.POINTER(_P),
                                      C.POINTER(AccelInfo)]),
@@ -388,6 +389,12 @@ class HipContext:
         self._check(self.lib.akr_hip_kernel_stats(self.h, C.cast(arr, C.c_void_p), n.value, C.byref(n)))
         return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms, min_ms=arr[i].min_ms,
                                            max_ms=arr[i].max_ms) for i in range(n.value)}
+
+    def render_info(self) -> dict:
+        """Lookahead lanes per pixel and sample passes of the last render."""
+        lanes, passes = C.c_int32(0), C.c_int32(0)
+        self._check(self.lib.akr_hip_render_info(self.h, C.byref(lanes), C.byref(passes)))
+        return {"lanes": lanes.value, "passes": passes.value}
 
     def trace_counts(self) -> dict:
         c = TraceCounts()

@@ -165,6 +165,39 @@ struct AoResolveArgs {
     float occlude;
 };
 
+// Lookahead lanes.  A lane of a pixel runs "the sample that starts o draws after
+// the pixel's committed sampler state" for one planned offset o; after the pass, the chain of lanes
+// whose offsets are real sample boundaries (0, then each accepted lane's end offset) is accepted.
+// The R pixels active in a pass each get look_lanes(R) lanes; slot j = lane * R + r for the r-th
+// active pixel.
+struct LookArgs {
+    const uint32_t *pixel;         // per pixel: x | y << 16
+    uint32_t n_pix, spp, budget, lane_cap;
+    uint32_t max_draws;            // a sample draws at most this many numbers (4 + 6 max_depth)
+    uint32_t nbins;                // sample-length histogram bins (length 4 + 2 b)
+    uint32_t width;
+    uint32_t *commit, *done;       // per pixel: sampler state at its first unfinished sample, samples done
+    uint8_t *hist;                 // per pixel: [kLookBins] u8 sample-length counts
+    const uint32_t *act;           // this pass: active pixels (indices), count *nact
+    const uint32_t *nact;
+    uint32_t *act_next, *nact_next;  // k_la_accept appends the pixels left for the next pass
+    uint32_t *off;                 // [lane * R + r]: planned offset (kNoOffset = no lane)
+    const uint32_t *seed;          // per slot: final sampler state (k_shade)
+    uint32_t *acc;                 // per active pixel: accepted lanes
+    uint32_t *chain;               // [t * R + r]: the t-th accepted lane
+};
+constexpr uint32_t kLookBins = 32;
+constexpr uint32_t kLookMaxLanes = 64;
+constexpr uint32_t kNoOffset = 0xFFFFFFFFu;
+
+// lanes per active pixel: min(cap, max(1, round(budget / R)))
+__host__ __device__ inline uint32_t look_lanes(uint32_t R, uint32_t budget, uint32_t cap) {
+    if (R == 0) return 0;
+    uint64_t l = ((uint64_t)budget + R / 2) / R;
+    if (l < 1) l = 1;
+    return (uint32_t)(l < cap ? l : cap);
+}
+
 struct RaygenArgs {
     CameraDev cam;
     const uint32_t *pixel;         // per slot: x | y << 16
@@ -176,6 +209,8 @@ struct RaygenArgs {
     uint32_t *slot_out;
     uint32_t *count_out;
     int32_t first_pass;
+    uint32_t lookahead;            // nonzero: k_raygen_lanes over the planned lanes of `look`
+    LookArgs look;
 };
 
 struct SplatArgs {
@@ -183,6 +218,8 @@ struct SplatArgs {
     float4 *film;
     uint32_t n;
     float ray_clamp;
+    uint32_t lookahead;            // nonzero: per active pixel of `look`, its accepted lanes in chain order
+    LookArgs look;
 };
 
 }  // namespace akr

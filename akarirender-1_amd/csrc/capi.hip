@@ -183,6 +183,17 @@ struct akr_hip_ctx {
     DBuf<float4> d_L[2];  // per-sample radiance, alternating by sample pass (passes overlap)
     DBuf<float4> d_sray[2], d_scolor[2];  // shadow queues, alternating by bounce
     DBuf<uint32_t> d_ao_slot[2];          // AO queues traced closest-hit (finite occlude): slots
+    // lookahead lanes: per pixel committed sampler state, samples done, sample-length
+    // histogram; per slot planned offset; per pass parity active list + count, accepted lanes, chain
+    DBuf<uint32_t> d_commit, d_done, d_off, d_act[2], d_acc[2], d_chain[2], d_nact;
+    DBuf<uint8_t> d_hist;
+    uint32_t *h_remain = nullptr;         // pinned, [2]: pixels left after the pass of that parity
+    hipEvent_t ev_acc[2] = {nullptr, nullptr}, ev_rem[2] = {nullptr, nullptr};
+    int lookahead = 1;                    // 1 = off (default), 0 = on when it adds lanes, >= 2: on, lane cap
+    int64_t slot_target = 2000000;        // lookahead budget: path slots per pass
+    uint64_t cur_slots = 0;               // path slots the buffers of the current render hold
+    bool cur_look = false;
+    int last_lanes = 1, last_passes = 0;
     // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
     // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
     // Both internal: `main` (high priority) runs raygen / closest-hit / shade, `side` (low priority)
@@ -227,8 +238,10 @@ struct akr_hip_ctx {
         for (auto e : pool) (void)hipEventDestroy(e);
         if (side) (void)hipStreamSynchronize(side);
         if (main_st) (void)hipStreamSynchronize(main_st);
-        for (hipEvent_t e : {ev_fork, ev_join, ev_join_main, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1]})
+        for (hipEvent_t e : {ev_fork, ev_join, ev_join_main, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1],
+                             ev_acc[0], ev_acc[1], ev_rem[0], ev_rem[1]})
             if (e) (void)hipEventDestroy(e);
+        if (h_remain) (void)hipHostFree(h_remain);
         if (main_st) (void)hipStreamDestroy(main_st);
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
@@ -400,8 +413,10 @@ struct akr_hip_ctx {
         HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPCHK(hipStreamCreateWithPriority(&main_st, hipStreamNonBlocking, greatest));
         HIPCHK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, least));
-        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_join_main, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1]})
+        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_join_main, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1],
+                              &ev_acc[0], &ev_acc[1], &ev_rem[0], &ev_rem[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_remain), 2 * sizeof(uint32_t), hipHostMallocDefault));
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
@@ -492,7 +507,9 @@ struct akr_hip_ctx {
 
     // Pixels of the tile list (tiles in order, row-major inside a tile) into h_pixel / d_pixel;
     // sizes the queues and the per-pass counter sets.  Returns the pixel count.
-    uint64_t setup_pixels(const akr_rect *tiles, int32_t n_tiles, size_t n_count_words, hipStream_t st) {
+    // look_ok: the render may use lookahead lanes (cur_look); the path buffers are sized for it.
+    uint64_t setup_pixels(const akr_rect *tiles, int32_t n_tiles, size_t n_count_words, hipStream_t st,
+                          bool look_ok = false) {
         require_ready();
         if (!cam_set) throw std::runtime_error("camera not set (call akr_hip_set_camera)");
         if (n_tiles < 0 || (n_tiles > 0 && !tiles)) throw std::runtime_error("invalid tile list");
@@ -505,7 +522,11 @@ struct akr_hip_ctx {
         }
         const uint64_t N = h_pixel.size();
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
-        ensure_capacity(N);
+        // lookahead: R active pixels get look_lanes(R) lanes, R * lanes <= max(N, budget + N / 2)
+        cur_look = look_ok && lookahead != 1 && look_lanes((uint32_t)N, look_budget(), look_cap()) >= 2;
+        cur_slots = cur_look ? std::max<uint64_t>(N, (uint64_t)look_budget() + N / 2) : N;
+        if (cur_slots >= (1ull << 31)) throw std::runtime_error("lookahead slot budget too large");
+        ensure_capacity(cur_slots);  // before any upload: a reallocation drops contents
         d_counts.reserve(2 * n_count_words);
         if (N == 0) return 0;
         ensure_side_stream();
@@ -543,17 +564,71 @@ struct akr_hip_ctx {
         return rg;
     }
 
+    uint32_t look_budget() const { return (uint32_t)std::min<int64_t>(slot_target, 1ll << 30); }
+    uint32_t look_cap() const { return lookahead >= 2 ? (uint32_t)lookahead : kLookMaxLanes; }
+
     uint64_t render(const akr_pt_params &p, const akr_rect *tiles, int32_t n_tiles, hipStream_t st) {
         if (p.spp < 0 || p.max_depth < 0) throw std::runtime_error("spp and max_depth must be >= 0");
         if (p.max_depth > 1000) throw std::runtime_error("max_depth too large");
         // counters per pass, each on its own 128-B line (atomics on one line serialise):
-        // M ray-queue counts, M shadow-queue counts, then 2 trace launches x kTraceWords per bounce;
+        // D ray-queue counts, D shadow-queue counts, 2 trace launches x kTraceWords per bounce;
         // two sets, alternating by pass, since consecutive passes overlap
-        const int M = p.max_depth + 2;
-        const size_t n_count_words = 2 * (size_t)M * kWorkStride + 2 * (size_t)M * kTraceWords;
-        const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st);
+        const int D = p.max_depth + 2;
+        const size_t n_count_words = 2 * (size_t)D * kWorkStride + 2 * (size_t)D * kTraceWords;
+        last_lanes = 1;
+        last_passes = 0;
+        // lookahead needs every sample length in the histogram's range: max_depth <= 10
+        const bool look_ok = p.spp >= 2 && 3u * (uint32_t)p.max_depth + 1u <= kLookBins;
+        const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st, look_ok);
         if (N == 0) return 0;
+        // Lookahead: lanes of a pixel run the samples that start at planned draw
+        // offsets from its committed sampler state; k_la_accept keeps the chain of lanes that start
+        // at real sample boundaries.  Slot j = lane * R + r over the pass's R active pixels.
+        const bool la = cur_look;
+        const uint64_t S = cur_slots;
         hipStream_t ms = main_st;
+        LookArgs lk{};
+        if (la) {
+            d_commit.reserve(N);
+            d_done.reserve(N);
+            d_hist.reserve(N * kLookBins);
+            d_off.reserve(S);
+            for (int k = 0; k < 2; k++) {
+                d_act[k].reserve(N);
+                d_acc[k].reserve(N);
+                d_chain[k].reserve(S);
+            }
+            d_nact.reserve(2 * kWorkStride);
+            lk.pixel = d_pixel.p;
+            lk.n_pix = (uint32_t)N;
+            lk.spp = (uint32_t)p.spp;
+            lk.budget = look_budget();
+            lk.lane_cap = look_cap();
+            lk.max_draws = 4u + 6u * (uint32_t)p.max_depth;
+            lk.nbins = 3u * (uint32_t)p.max_depth + 1u;
+            lk.width = (uint32_t)cam.width;
+            lk.commit = d_commit.p;
+            lk.done = d_done.p;
+            lk.hist = d_hist.p;
+            lk.off = d_off.p;
+            lk.seed = d_seed.p;
+            last_lanes = (int)look_lanes((uint32_t)N, lk.budget, lk.lane_cap);
+        }
+        // the lookahead arguments of the pass with parity q (its active list, acceptance record)
+        auto look = [&](int q) {
+            LookArgs x = lk;
+            x.act = d_act[q].p;
+            x.nact = d_nact.p + (size_t)q * kWorkStride;
+            x.act_next = d_act[q ^ 1].p;
+            x.nact_next = d_nact.p + (size_t)(q ^ 1) * kWorkStride;
+            x.acc = d_acc[q].p;
+            x.chain = d_chain[q].p;
+            return x;
+        };
+        if (la) {
+            timed("la_init", ms, [&] { launch_la_init(lk, d_act[0].p, d_nact.p, ms); });
+            timed("la_plan", ms, [&] { launch_la_plan(look(0), (uint32_t)N, ms); });
+        }
         const SceneDev sd = scene_dev();
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
@@ -561,15 +636,26 @@ struct akr_hip_ctx {
         int64_t g = 0;  // bounce index over all passes: shadow queues alternate by its parity
         for (int s = 0; s < p.spp; s++) {
             const int ps = s & 1;
+            // lookahead: stop once the pass before last finished every pixel (the last pass then
+            // found nothing to do); the host stays two passes ahead of the device
+            if (la && s >= 2) {
+                HIPCHK(hipEventSynchronize(ev_rem[ps]));
+                if (h_remain[ps] == 0) break;
+            }
+            last_passes++;
             uint32_t *cnt = d_counts.p + (size_t)ps * n_count_words;
             auto qcount = [&](int b) { return cnt + (size_t)b * kWorkStride; };
-            auto scount = [&](int b) { return cnt + (size_t)(M + b) * kWorkStride; };
-            auto work = [&](int b, int k) { return cnt + 2 * (size_t)M * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
+            auto scount = [&](int b) { return cnt + (size_t)(D + b) * kWorkStride; };
+            auto work = [&](int b, int k) { return cnt + 2 * (size_t)D * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
             float4 *L = d_L[ps].p;
             // L[ps] and the counter set were last used by pass s - 2, whose splat ends its side-stream work
             if (s >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ps], 0));
             HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
-            const RaygenArgs rg = raygen_args((uint32_t)N, L, qcount(0), s == 0);
+            RaygenArgs rg = raygen_args(la ? (uint32_t)S : (uint32_t)N, L, qcount(0), s == 0);
+            if (la) {
+                rg.lookahead = 1;
+                rg.look = look(ps);
+            }
             timed("raygen", ms, [&] { launch_raygen(rg, ms); });
             for (int b = 0; b < nb; b++, g++) {
                 const bool odd = b & 1;
@@ -578,7 +664,7 @@ struct akr_hip_ctx {
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
-                timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
+                timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, S, ms); });
                 // shade refills shadow queue g % 2: the shadow trace of bounce g - 2 must be done
                 if (g >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_shadow[sq], 0));
                 ShadeArgs sh{};
@@ -600,7 +686,7 @@ struct akr_hip_ctx {
                 sh.depth = b;
                 sh.max_depth = p.max_depth;
                 sh.last = b == nb - 1;
-                timed("shade", ms, [&] { launch_shade(sh, (uint32_t)N, ms); });
+                timed("shade", ms, [&] { launch_shade(sh, (uint32_t)S, ms); });
                 HIPCHK(hipEventRecord(ev_shade[sq], ms));
                 HIPCHK(hipStreamWaitEvent(side, ev_shade[sq], 0));
                 if (b < p.max_depth) {
@@ -610,18 +696,34 @@ struct akr_hip_ctx {
                     ts.count = scount(b);
                     ts.shadow_color = d_scolor[sq].p;
                     ts.L = L;
-                    timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, side); });
+                    timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, S, side); });
                 }
                 HIPCHK(hipEventRecord(ev_shadow[sq], side));
             }
+            SplatArgs sp{};
+            if (la) {
+                // every lane's final sampler state is written by the pass's last shade; the next
+                // pass's active list (parity ps ^ 1) was last read by the splat of pass s - 1
+                const int ns = ps ^ 1;
+                if (s >= 1) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ns], 0));
+                HIPCHK(hipMemsetAsync(d_nact.p + (size_t)ns * kWorkStride, 0, sizeof(uint32_t), ms));
+                timed("la_accept", ms, [&] { launch_la_accept(look(ps), (uint32_t)N, ms); });
+                HIPCHK(hipMemcpyAsync(&h_remain[ps], d_nact.p + (size_t)ns * kWorkStride, sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, ms));
+                HIPCHK(hipEventRecord(ev_rem[ps], ms));
+                HIPCHK(hipEventRecord(ev_acc[ps], ms));
+                HIPCHK(hipStreamWaitEvent(side, ev_acc[ps], 0));
+                timed("la_plan", ms, [&] { launch_la_plan(look(ns), (uint32_t)N, ms); });
+                sp.lookahead = 1;
+                sp.look = look(ps);
+            }
             // Tile::add_sample on the side stream, after the pass's last shadow trace: the next
             // pass (its own L and counters) proceeds on the main stream meanwhile
-            SplatArgs sp{};
             sp.L = L;
             sp.film = d_film.p;
             sp.n = (uint32_t)N;
             sp.ray_clamp = p.ray_clamp;
-            timed("splat", side, [&] { launch_splat(sp, side); });
+            timed("splat", side, [&] { launch_splat(sp, (uint32_t)N, side); });
             HIPCHK(hipEventRecord(ev_splat[ps], side));
         }
         join_streams(st);
@@ -695,7 +797,7 @@ struct akr_hip_ctx {
             sp.film = d_film.p;
             sp.n = (uint32_t)N;
             sp.ray_clamp = 0.0f;  // Tile::add_sample(p, L, 1) unclamped (integrator.cpp:78)
-            timed("splat", side, [&] { launch_splat(sp, side); });
+            timed("splat", side, [&] { launch_splat(sp, (uint32_t)N, side); });
             HIPCHK(hipEventRecord(ev_splat[ps], side));
         }
         join_streams(st);
@@ -777,6 +879,13 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "shadow_grid_pct") {
             if (value < 1 || value > 100) throw std::runtime_error("shadow_grid_pct must be in [1, 100]");
             ctx->shadow_grid_pct = (int)value;
+        } else if (k == "lookahead") {
+            if (value < 0 || value > (int64_t)kLookMaxLanes)
+                throw std::runtime_error("lookahead must be in [0, 64] (0 = auto, 1 = off, n = on with at most n lanes)");
+            ctx->lookahead = (int)value;
+        } else if (k == "slot_target") {
+            if (value < 1) throw std::runtime_error("slot_target must be >= 1");
+            ctx->slot_target = value;
         } else if (k == "rays_per_lane") {
             if (value < 1 || value > 64) throw std::runtime_error("rays_per_lane must be in [1, 64]");
             ctx->rays_per_lane = (int)value;
@@ -1175,6 +1284,13 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
             out->lane_slots[m][2] = c[m].slots_tri;
             out->lane_slots[m][3] = c[m].visits;
         }
+    });
+}
+
+int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes) {
+    return guard(ctx, [&] {
+        if (lanes) *lanes = ctx->last_lanes;
+        if (passes) *passes = ctx->last_passes;
     });
 }
 

@@ -11,7 +11,10 @@ void launch_trace(int mode, bool count, bool tight, bool wide, const TraceArgs &
 int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);
-void launch_splat(const SplatArgs &a, hipStream_t st);
+void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st);
+void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st);
+void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st);
+void launch_la_accept(const LookArgs &a, uint32_t max_active, hipStream_t st);
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t st);
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st);

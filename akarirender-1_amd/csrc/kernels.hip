@@ -3,10 +3,12 @@
 //   k_trace<MODE,...>  BVH2 traversal, one ray per lane, LDS-resident stack, persistent waves that
 //                      refill idle lanes from the queue (TBVHAccelerator::intersect / occlude,
 //                      bvh-accelerator.h:488-547)
-//   k_raygen           camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86)
+//   k_raygen           camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86);
+//                      k_la_plan / k_raygen_lanes / k_la_accept: lookahead lanes (several samples of a pixel in
+//                      flight from predicted sampler states, accepted when the prediction held)
 //   k_shade            hit -> emission / BSDF sample / NEE light sample, wave-ballot compaction
 //                      of live paths and shadow rays (pathtracer.h:69-132, 137-162)
-//   k_splat            Tile::add_sample per slot (core/film.h:66-70)
+//   k_splat            Tile::add_sample per pixel, in sample order (core/film.h:66-70)
 //
 // Numerics: f32 with the reference's operation order (akr_math.h); the library is built with
 // -ffp-contract=off and correctly rounded division/sqrt.
@@ -729,18 +731,13 @@ __device__ __forceinline__ void apply_rows(const float *m, float x, float y, flo
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t px = a.pixel[i];
-    const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
-    uint32_t seed = a.first_pass ? (uint32_t)(x + y * a.cam.width) : a.seed[i];
-    // camera_ray: generate_ray(next2d() /*lens*/, next2d() /*film*/, p) — pathtracer.h:61-64
+// camera_ray: generate_ray(next2d() /*lens*/, next2d() /*film*/, p) — pathtracer.h:61-64
+__device__ __forceinline__ void camera_ray(const CameraDev &cam, int x, int y, uint32_t &seed, float4 &r0, float4 &r1) {
     lcg_next2(seed);
     const V2 u2 = lcg_next2(seed);
     const float pfx = (float)x + u2.x, pfy = (float)y + u2.y;
     float r[4];
-    apply_rows(a.cam.r2c, pfx, pfy, 0.0f, 1.0f, r, 4);  // Transform::apply_point, math.h:243-251
+    apply_rows(cam.r2c, pfx, pfy, 0.0f, 1.0f, r, 4);  // Transform::apply_point, math.h:243-251
     float px_ = r[0], py_ = r[1];
     if (r[3] != 1.0f) {
         px_ = px_ / r[3];
@@ -748,22 +745,264 @@ __global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
     }
     V3 d = normalize(v3(px_ - 0.0f, py_ - 0.0f, 0.0f - 1.0f));
     float ro[4];
-    apply_rows(a.cam.c2w, 0.0f, 0.0f, 0.0f, 1.0f, ro, 4);
+    apply_rows(cam.c2w, 0.0f, 0.0f, 0.0f, 1.0f, ro, 4);
     V3 o = v3(ro[0], ro[1], ro[2]);
     if (ro[3] != 1.0f) o = divs(o, ro[3]);
     float rd[3];
     for (int k = 0; k < 3; k++) {  // apply_vector: m3 * v, math.h:253
-        float s = a.cam.c2w[4 * k + 0] * d.x;
-        s += a.cam.c2w[4 * k + 1] * d.y;
-        s += a.cam.c2w[4 * k + 2] * d.z;
+        float s = cam.c2w[4 * k + 0] * d.x;
+        s += cam.c2w[4 * k + 1] * d.y;
+        s += cam.c2w[4 * k + 2] * d.z;
         rd[k] = s;
     }
+    r0 = make_float4(o.x, o.y, o.z, kEps);
+    r1 = make_float4(rd[0], rd[1], rd[2], kInf);
+}
+
+__global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t px = a.pixel[i];
+    const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
+    uint32_t seed = a.first_pass ? (uint32_t)(x + y * a.cam.width) : a.seed[i];
+    float4 r0, r1;
+    camera_ray(a.cam, x, y, seed, r0, r1);
     a.L[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    a.ray_out[2 * (size_t)i] = make_float4(o.x, o.y, o.z, kEps);
-    a.ray_out[2 * (size_t)i + 1] = make_float4(rd[0], rd[1], rd[2], kInf);
+    a.ray_out[2 * (size_t)i] = r0;
+    a.ray_out[2 * (size_t)i + 1] = r1;
     a.state_out[i] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
     a.slot_out[i] = i;
     if (i == 0) *a.count_out = a.n;
+}
+
+// LCG state after n draws: the affine step s -> A s + C raised to the n-th power by squaring
+__device__ __forceinline__ uint32_t lcg_advance(uint32_t s, uint32_t n) {
+    uint32_t A = 1103515245u, C = 12345u, ra = 1u, rc = 0u;
+    while (n) {
+        if (n & 1u) {
+            ra = A * ra;
+            rc = A * rc + C;
+        }
+        C = A * C + C;
+        A = A * A;
+        n >>= 1;
+    }
+    return ra * s + rc;
+}
+
+// ------------------------------------------------------------------------------- lookahead
+// DESIGN.md §3.7.  A pixel's samples are sequential only through its sampler state: sample s + 1
+// starts where sample s stopped drawing (cpu/integrator.cpp:124-134), and a sample draws 4 + 6 k
+// (+2) numbers for k scattering events.  A lane runs the sample starting o draws after the pixel's
+// committed state for a planned offset o; the lanes whose offsets turn out to be real sample
+// boundaries are exactly the sequential samples, so accepting the chain 0 -> end(0) -> ... keeps
+// every result bit-identical to the sequential loop.
+
+// Per pixel: committed state x + y W (the reference seed), no samples, empty length histogram;
+// pass 0's active list is every pixel.
+__global__ __launch_bounds__(kBlock) void k_la_init(LookArgs a, uint32_t *act0, uint32_t *nact0) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n_pix) return;
+    const uint32_t px = a.pixel[i];
+    a.commit[i] = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * (int)a.width);
+    a.done[i] = 0;
+    uint4 *h = reinterpret_cast<uint4 *>(a.hist + (size_t)i * kLookBins);
+    h[0] = make_uint4(0, 0, 0, 0);
+    h[1] = make_uint4(0, 0, 0, 0);
+    act0[i] = i;
+    if (i == 0) *nact0 = a.n_pix;
+}
+
+// Plans the lanes of each active pixel.  From its sample-length histogram take the m most frequent
+// lengths c_1..c_m (total frequency q_m); the offsets are every sum of at most d of them (a chain of
+// t samples whose lengths are all among the m is then accepted in full), with (m, d) maximising the
+// expected accepted chain sum_{t=1..d} q_m^t under C(d + m, m) <= lanes and d < samples left.
+// Without history: lengths 4 (camera miss) and max_draws (full-length path), equally likely.
+__global__ __launch_bounds__(kBlock) void k_la_plan(LookArgs a) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t R = *a.nact;
+    if (r >= R) return;
+    const uint32_t L = look_lanes(R, a.budget, a.lane_cap);
+    const uint32_t pix = a.act[r];
+    const uint32_t rem = a.spp - a.done[pix];
+    constexpr int kTop = 6;
+    uint32_t c[kTop];
+    float p[kTop];
+    int mav = 0;
+    {
+        const uint4 *hp = reinterpret_cast<const uint4 *>(a.hist + (size_t)pix * kLookBins);
+        const uint4 h0 = hp[0], h1 = hp[1];
+        uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        uint32_t total = 0;
+        for (int b = 0; b < (int)kLookBins; b++) total += (w[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+        if (total == 0) {
+            c[0] = 4u;
+            p[0] = 1.0f;
+            mav = 1;
+            if (a.max_draws != 4u) {
+                c[1] = a.max_draws;
+                p[0] = p[1] = 0.5f;
+                mav = 2;
+            }
+        } else {
+            for (; mav < kTop; mav++) {
+                uint32_t best = 0, bb = 0;
+                for (int b = 0; b < (int)kLookBins; b++) {
+                    const uint32_t v = (w[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+                    if (v > best) {
+                        best = v;
+                        bb = (uint32_t)b;
+                    }
+                }
+                if (best == 0) break;
+                w[bb >> 2] &= ~(0xFFu << (8 * (bb & 3)));
+                c[mav] = 4u + 2u * bb;
+                p[mav] = (float)best / (float)total;
+            }
+        }
+    }
+    int bm = 1, bd = 0;
+    float be = -1.0f, q = 0.0f;
+    for (int m = 1; m <= mav; m++) {
+        q += p[m - 1];
+        uint64_t need = 1;  // C(d + m, m) lanes for depth d
+        int d = 0;
+        while ((uint32_t)d + 1 < rem) {
+            const uint64_t nx = need * (uint64_t)(d + 1 + m) / (uint64_t)(d + 1);
+            if (nx > L) break;
+            need = nx;
+            d++;
+        }
+        float e = 0.0f, qt = 1.0f;
+        for (int t = 1; t <= d; t++) {
+            qt *= q;
+            e += qt;
+        }
+        if (e > be * 1.0001f) {
+            be = e;
+            bm = m;
+            bd = d;
+        }
+    }
+    // breadth-first over multisets (non-decreasing length index); a repeated sum is one lane
+    uint32_t o[kLookMaxLanes];
+    uint8_t last[kLookMaxLanes];
+    uint32_t n = 1, lb = 0, le = 1;
+    o[0] = 0;
+    last[0] = 0;
+    for (int t = 1; t <= bd && n < L; t++) {
+        for (uint32_t e = lb; e < le && n < L; e++)
+            for (int i = last[e]; i < bm && n < L; i++) {
+                const uint32_t v = o[e] + c[i];
+                bool dup = false;
+                for (uint32_t k = 0; k < n; k++) dup = dup || o[k] == v;
+                if (dup) continue;
+                o[n] = v;
+                last[n] = (uint8_t)i;
+                n++;
+            }
+        lb = le;
+        le = n;
+    }
+    for (uint32_t k = 0; k < L; k++) a.off[(size_t)k * R + r] = k < n ? o[k] : kNoOffset;
+}
+
+// Lookahead raygen: one thread per planned lane (slot j = lane * R + r); camera ray of the sample
+// that starts at the lane's offset.
+__global__ __launch_bounds__(kBlock) void k_raygen_lanes(RaygenArgs a) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t R = *a.look.nact;
+    const uint32_t n = R * look_lanes(R, a.look.budget, a.look.lane_cap);
+    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup: before the barrier
+    bool want = false;
+    float4 r0 = {}, r1 = {};
+    uint32_t seed = 0;
+    if (j < n) {
+        const uint32_t o = a.look.off[j];
+        if (o != kNoOffset) {
+            const uint32_t pix = a.look.act[j % R];
+            const uint32_t px = a.pixel[pix];
+            seed = lcg_advance(a.look.commit[pix], o);
+            camera_ray(a.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, r0, r1);
+            a.L[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            want = true;
+        }
+    }
+    uint32_t pos, unused;
+    block_append2(want, a.count_out, pos, false, a.count_out, unused);
+    if (want) {
+        a.ray_out[2 * (size_t)pos] = r0;
+        a.ray_out[2 * (size_t)pos + 1] = r1;
+        a.state_out[pos] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
+        a.slot_out[pos] = j;
+    }
+}
+
+// After the pass's last shade (every lane's final sampler state written), per active pixel: each
+// lane's sample length (steps from its start state to its final state), the histogram update, the
+// accepted chain, the new committed state and the next pass's active list.
+__global__ __launch_bounds__(kBlock) void k_la_accept(LookArgs a) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t R = *a.nact;
+    if (blockIdx.x * kBlock >= R) return;  // uniform per workgroup: before the barrier
+    bool left = false;
+    uint32_t pix = 0;
+    if (r < R) {
+        const uint32_t L = look_lanes(R, a.budget, a.lane_cap);
+        pix = a.act[r];
+        const uint32_t base = a.commit[pix];
+        uint4 *hp = reinterpret_cast<uint4 *>(a.hist + (size_t)pix * kLookBins);
+        const uint4 h0 = hp[0], h1 = hp[1];
+        uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        uint32_t o[kLookMaxLanes], e[kLookMaxLanes];
+        uint32_t n = 0;
+        for (uint32_t k = 0; k < L; k++) {
+            const uint32_t ok = a.off[(size_t)k * R + r];
+            if (ok == kNoOffset) break;
+            const uint32_t f = a.seed[(size_t)k * R + r];
+            uint32_t s = lcg_advance(base, ok), len = kNoOffset;
+            for (uint32_t d = 1; d <= a.max_draws; d++) {
+                s = 1103515245u * s + 12345u;
+                if (s == f) {
+                    len = d;
+                    break;
+                }
+            }
+            o[n] = ok;
+            e[n] = len == kNoOffset ? kNoOffset : ok + len;
+            n++;
+            if (len != kNoOffset && len >= 4u && !(len & 1u) && (len - 4u) / 2u < a.nbins) {
+                const uint32_t b = (len - 4u) / 2u, sh = 8 * (b & 3);
+                if (((w[b >> 2] >> sh) & 0xFFu) == 0xFFu)  // saturated: halve every count
+                    for (int q = 0; q < 8; q++) w[q] = (w[q] >> 1) & 0x7F7F7F7Fu;
+                w[b >> 2] += 1u << sh;
+            }
+        }
+        hp[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        hp[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        const uint32_t done = a.done[pix], rem = a.spp - done;
+        uint32_t cur = 0, acc = 1;
+        a.chain[r] = 0;
+        while (acc < rem && e[cur] != kNoOffset) {
+            uint32_t nx = kNoOffset;
+            for (uint32_t k = 1; k < n; k++)
+                if (o[k] == e[cur]) {
+                    nx = k;
+                    break;
+                }
+            if (nx == kNoOffset) break;
+            a.chain[(size_t)acc * R + r] = nx;
+            acc++;
+            cur = nx;
+        }
+        a.commit[pix] = a.seed[(size_t)cur * R + r];
+        a.done[pix] = done + acc;
+        a.acc[r] = acc;
+        left = done + acc < a.spp;
+    }
+    uint32_t pos, unused;
+    block_append2(left, a.nact_next, pos, false, a.nact_next, unused);
+    if (left) a.act_next[pos] = pix;
 }
 
 // ------------------------------------------------------------------------------------- shade
@@ -999,24 +1238,41 @@ __global__ __launch_bounds__(kBlock) void k_ao_resolve(AoResolveArgs a) {
 }
 
 // ------------------------------------------------------------------------------------- splat
-__global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const float4 l = a.L[i];
+__device__ __forceinline__ void splat_one(float4 &f, float4 l, float ray_clamp) {
     float r = l.x, g = l.y, b = l.z;
-    if (a.ray_clamp > 0.0f) {  // clamp_zero + min (gpu/cuda/integrator.cpp:397-398)
+    if (ray_clamp > 0.0f) {  // clamp_zero + min (gpu/cuda/integrator.cpp:397-398)
         r = isnan(r) ? 0.0f : rmax(0.0f, r);
         g = isnan(g) ? 0.0f : rmax(0.0f, g);
         b = isnan(b) ? 0.0f : rmax(0.0f, b);
-        r = rmin(r, a.ray_clamp);
-        g = rmin(g, a.ray_clamp);
-        b = rmin(b, a.ray_clamp);
+        r = rmin(r, ray_clamp);
+        g = rmin(g, ray_clamp);
+        b = rmin(b, ray_clamp);
     }
-    float4 f = a.film[i];
     f.x += r;
     f.y += g;
     f.z += b;
     f.w += 1.0f;
+}
+
+// Tile::add_sample per pixel, in sample order (lookahead: each active pixel's accepted lanes in
+// chain order)
+__global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (a.lookahead) {
+        const uint32_t R = *a.look.nact;
+        if (i >= R) return;
+        const uint32_t pix = a.look.act[i], acc = a.look.acc[i];
+        float4 f = a.film[pix];
+        for (uint32_t t = 0; t < acc; t++) {
+            const uint32_t k = a.look.chain[(size_t)t * R + i];
+            splat_one(f, a.L[(size_t)k * R + i], a.ray_clamp);
+        }
+        a.film[pix] = f;
+        return;
+    }
+    if (i >= a.n) return;
+    float4 f = a.film[i];
+    splat_one(f, a.L[i], a.ray_clamp);
     a.film[i] = f;
 }
 
@@ -1071,12 +1327,28 @@ int trace_blocks_per_cu(int mode) {
 }
 
 void launch_raygen(const RaygenArgs &a, hipStream_t st) {
+    if (a.lookahead) {  // a.n: the slot capacity (the device decides how many are planned)
+        if (a.n) hipLaunchKernelGGL(k_raygen_lanes, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
+        return;
+    }
     if (a.n == 0) return;
     hipLaunchKernelGGL(k_raygen, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
 }
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_shade, dim3((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock)), dim3(kShadeBlock), 0, st, a);
+}
+void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st) {
+    if (a.n_pix == 0) return;
+    hipLaunchKernelGGL(k_la_init, dim3(blocks_for(a.n_pix)), dim3(kBlock), 0, st, a, act0, nact0);
+}
+void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st) {
+    if (max_active == 0) return;
+    hipLaunchKernelGGL(k_la_plan, dim3(blocks_for(max_active)), dim3(kBlock), 0, st, a);
+}
+void launch_la_accept(const LookArgs &a, uint32_t max_active, hipStream_t st) {
+    if (max_active == 0) return;
+    hipLaunchKernelGGL(k_la_accept, dim3(blocks_for(max_active)), dim3(kBlock), 0, st, a);
 }
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
@@ -1086,9 +1358,9 @@ void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t s
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_ao_resolve, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
-void launch_splat(const SplatArgs &a, hipStream_t st) {
-    if (a.n == 0) return;
-    hipLaunchKernelGGL(k_splat, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
+void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items == 0) return;
+    hipLaunchKernelGGL(k_splat, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
     if (n == 0) return;

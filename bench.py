@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--shadow-grid-pct", type=int, default=100, help="tuning: shadow-trace grid, %% of resident max")
     ap.add_argument("--timed-stats", type=int, default=1,
                     help="per-kernel HIP events inside the timed region (0: probe their overhead)")
+    ap.add_argument("--lookahead", type=int, default=1,
+                    help="speculative sample lanes per pixel (1 = off, 0 = on from --slot-target, n = at most n lanes)")
+    ap.add_argument("--slot-target", type=int, default=0, help="auto lookahead: path slots per render (0: library default)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -110,6 +113,9 @@ def main():
     ctx.set_option("wide", args.wide)
     if not args.lean:
         ctx.set_option("lean", 0)
+    ctx.set_option("lookahead", args.lookahead)
+    if args.slot_target:
+        ctx.set_option("slot_target", args.slot_target)
     if args.shadow_grid_pct != 100:
         ctx.set_option("shadow_grid_pct", args.shadow_grid_pct)
     log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
@@ -160,6 +166,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kstats = ctx.kernel_stats()
+    la = ctx.render_info()
 
     # sanity: every pixel of this rank got K samples
     assert int(wgt[:npix].min().item()) == K and int(wgt[:npix].max().item()) == K
@@ -172,7 +179,7 @@ def main():
     if split != world:  # scaling probe: one rank's share of an N-way split, on this GPU
         print(json.dumps({"probe": "emulated rank 0 of a tile split", "emulate_world": split, "rank_pixels": npix,
                           "rank_ms_per_step": round(elapsed / K * 1e3, 3),
-                          "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3),
+                          "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3), "lookahead": la,
                           "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3),
                           "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                                       for k, v in kstats.items()},
@@ -238,7 +245,7 @@ def main():
         "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)", "triangles": cs.n_tris,
                    "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
                    "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
-                   "sah_isect": args.sah_isect, "builder": args.builder},
+                   "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la},
         "roofline": roofline, "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                     for k, v in kstats.items()},

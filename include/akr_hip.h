@@ -173,7 +173,10 @@ int akr_hip_create(int device, akr_hip_ctx **out);
 int akr_hip_destroy(akr_hip_ctx *ctx);
 const char *akr_hip_last_error(const akr_hip_ctx *ctx);
 /* Options: "stats" (per-kernel HIP-event timing on/off), "count_tests" (traversal counters),
- * "stack_lds" (read-only). */
+ * "exact_cull", "wide", "lean", "shadow_grid_pct", "rays_per_lane" (tuning / A-B),
+ * "lookahead" (speculative sample lanes per pixel, DESIGN.md §3.7: 1 = off (default), 0 = on
+ * whenever "slot_target" gives a pixel two or more lanes, 2..64 = on with at most that many lanes;
+ * results are identical for every value), "slot_target" (lookahead path slots per pass). */
 int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value);
 
 int akr_hip_upload_mesh(akr_hip_ctx *ctx, const float *vertices, uint64_t n_vertices,
@@ -244,6 +247,8 @@ const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h);
 int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n);
 int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
+/* The last akr_hip_render's lookahead lanes per pixel and sample passes launched (diagnostic). */
+int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
 int akr_hip_synchronize(akr_hip_ctx *ctx);
 /* Diagnostic: with option "ray_steps" set, each standalone trace (akr_hip_trace /
  * akr_hip_trace_device) runs the counting kernel and records, per ray, the traversal-loop

@@ -146,6 +146,7 @@ def test_trace_each_ray_once(hip_ctx_factory, n):
         cs, orc = _setup(ctx, small_soup(20_000))
         rays = random_rays(n, 7, -1.1, 1.1)
         ctx.set_option("count_tests", 1)
+        ctx.set_option("lookahead", 1)   # no speculative lanes: exactly the sequential rays
         for any_hit in (False, True):
             ctx.reset_stats()
             ctx.trace(rays, any_hit=any_hit)
@@ -167,12 +168,66 @@ def _check_render(ctx, orc, spp, depth, tiles, W, H, clamp=0.0, exact=False):
     return rad, w
 
 
+@pytest.mark.parametrize("lookahead", [1, 0])
 @pytest.mark.parametrize("exact", [False, True])
-def test_render_cornell_bit_exact(hip_ctx_factory, exact):
+def test_render_cornell_bit_exact(hip_ctx_factory, exact, lookahead):
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, cornell((64, 64)))
+        ctx.set_option("lookahead", lookahead)
         rad, w = _check_render(ctx, orc, 16, 5, [(0, 0, 64, 64)], 64, 64, exact=exact)
         assert np.all(w == 16) and rad.mean() > 0
+        info = ctx.render_info()
+        assert info["lanes"] == (1 if lookahead == 1 else 64)   # auto: the 64-lane cap for 4,096 pixels
+        assert info["passes"] <= 16
+
+
+@pytest.mark.parametrize("lookahead", [2, 3, 8, 64])
+def test_render_lookahead_bit_exact(hip_ctx_factory, lookahead):
+    """Lookahead lanes: lanes run the samples that start at planned draw offsets
+    from a pixel's committed sampler state; only the chain of lanes starting at real sample
+    boundaries is splatted, so every lane count gives the sequential image bit for bit.  spp not
+    divisible by the lanes, fewer samples than lanes, ragged tiles, depth 0 (every sample draws 4
+    numbers: all lanes accepted), depth 1/2/5 and the clamp."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((40, 24)))
+        ctx.set_option("lookahead", lookahead)
+        tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]
+        for spp, depth in ((13, 5), (2, 5), (7, 0), (5, 1), (9, 2)):
+            _check_render(ctx, orc, spp, depth, tiles, 40, 24)
+            info = ctx.render_info()
+            assert info["lanes"] == lookahead and info["passes"] <= spp
+            if depth == 0:   # constant sample length: the planned chain is all accepted
+                assert info["passes"] <= -(-spp // lookahead) + 2
+        _check_render(ctx, orc, 6, 5, tiles, 40, 24, clamp=10.0)
+        # repeated renders reuse the lane buffers (no state may leak from the previous render)
+        _check_render(ctx, orc, 11, 5, [(0, 0, 40, 24)], 40, 24)
+
+
+def test_render_lookahead_budget_growth(hip_ctx_factory):
+    """A slot budget of 1.6 pixels per pixel: 2 lanes per pixel while all are active, more lanes
+    per remaining pixel as pixels finish (the lane count per pass follows the active count)."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, small_soup(50_000, (64, 36)))
+        ctx.set_option("lookahead", 0)
+        ctx.set_option("slot_target", int(1.6 * 64 * 36))
+        _check_render(ctx, orc, 16, 5, [(0, 0, 64, 36)], 64, 36)
+        info = ctx.render_info()
+        assert info["lanes"] == 2 and info["passes"] < 16
+
+
+def test_render_lookahead_soup_and_node(hip_ctx_factory):
+    with hip_ctx_factory(0) as ctx, hip_ctx_factory(0) as other:
+        cs, orc = _setup(ctx, small_soup(50_000, (64, 36)))
+        for la in (1, 4):
+            ctx.set_option("lookahead", la)
+            _check_render(ctx, orc, 12, 5, [(0, 0, 64, 36)], 64, 36)
+        # render_node with a different lane count per context gives the same image
+        scene.upload_scene(other, cs)
+        other.set_option("lookahead", 3)
+        tiles = [(x, y, x + 16, y + 12) for y in range(0, 36, 12) for x in range(0, 64, 16)]
+        ref, wref = ctx.render(7, 5, tiles, 64, 36)
+        rad, w = capi.render_node([ctx, other], 7, 5, tiles, 64, 36)
+        assert np.array_equal(w, wref) and np.array_equal(rad, ref)
 
 
 def test_render_tiles_depths_clamp(hip_ctx_factory):
