@@ -22,6 +22,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "akarirender-1_amd"))
 
 METRIC = "Msamples/sec (whole node), 10M-tri scene 1080p 1024spp, 1/2/4/8 MI355X"
+METRIC_CORNELL = "Msamples/sec, Cornell box 1080p 1024spp, 1x MI355X (BASELINE.json configs[1])"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic bytes per ray / AABB / triangle test
 
@@ -60,6 +61,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", choices=["soup", "cornell"], default="soup",
+                    help="soup: C3, the headline workload; cornell: C2 (BASELINE.json configs[1], the reference's "
+                         "Cornell box at 1080p on one GPU; a side measurement, not the driver's line)")
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -101,7 +105,10 @@ def main():
 
     W, H, K, Wm = args.width, args.height, args.steps, args.warmup
     t0 = time.time()
-    sc = scene.soup_scene(n_tris=args.tris, resolution=(W, H))
+    if args.scene == "cornell":
+        sc = scene.cornell_scene(ROOT / "tests" / "golden" / "CornellBox-Original.obj.mesh", resolution=(W, H))
+    else:
+        sc = scene.soup_scene(n_tris=args.tris, resolution=(W, H))
     cs = scene.compile_scene(sc)
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
@@ -118,7 +125,7 @@ def main():
         ctx.set_option("slot_target", args.slot_target)
     if args.shadow_grid_pct != 100:
         ctx.set_option("shadow_grid_pct", args.shadow_grid_pct)
-    log(f"[rank {rank}] soup {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
+    log(f"[rank {rank}] {args.scene} {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 
     split = args.emulate_world if (args.emulate_world > 1 and world == 1) else world
@@ -239,10 +246,11 @@ def main():
                "value_tight_cull": round(cpx * args.cpu_spp / dt_tight / 1e6, 4)}
 
     line = {
-        "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
+        "metric": METRIC if args.scene == "soup" else METRIC_CORNELL, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
         "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)", "triangles": cs.n_tris,
+        "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)" if args.scene == "soup" else
+                   "C2 Cornell box (reference fixture CornellBox-Original.obj.mesh, SURVEY.md §8d)", "triangles": cs.n_tris,
                    "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
                    "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
                    "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la},
