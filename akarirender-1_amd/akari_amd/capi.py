@@ -62,7 +62,7 @@ class Rect(C.Structure):
 class BuildParams(C.Structure):
     _fields_ = [("max_leaf_size", C.c_int32), ("n_bins", C.c_int32), ("traversal_cost", C.c_float),
                 ("intersect_cost", C.c_float), ("n_threads", C.c_int32), ("builder", C.c_int32),
-                ("_pad", C.c_int32 * 2)]
+                ("spatial_budget", C.c_float), ("_pad", C.c_int32)]
 
 
 class AccelInfo(C.Structure):
@@ -83,7 +83,7 @@ class TraceCounts(C.Structure):
 
 TEX_CONSTANT, TEX_IMAGE = 0, 1
 PT_EXACT_CULL = 1
-BUILDER_SAH, BUILDER_LBVH = 0, 1
+BUILDER_SAH, BUILDER_LBVH, BUILDER_SBVH = 0, 1, 2
 MAT_DIFFUSE, MAT_GLOSSY, MAT_EMISSIVE, MAT_MIX = 0, 1, 2, 3
 
 # numpy views of the POD structs (for vectorised ray/hit buffers)
@@ -168,13 +168,14 @@ def device_count() -> int:
 
 
 def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0,
-                   n_threads=0, wide=False):
+                   n_threads=0, wide=False, builder=0, spatial_budget=0.0):
     """Run the product BVH builder on the host (no device): returns (nodes, tris, info), plus
-    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide`."""
+    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide`.  builder: BUILDER_SAH
+    or BUILDER_SBVH (the host builders)."""
     lib = load_library()
     v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
     i = np.ascontiguousarray(indices, np.int32).reshape(-1)
-    p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads)
+    p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget)
     h = C.c_void_p()
     info = AccelInfo()
     st = lib.akr_bvh_host_build(_ptr(v), v.size // 3, _ptr(i), i.size // 3, C.byref(p), C.byref(h), C.byref(info))
@@ -299,9 +300,10 @@ class HipContext:
         self._check(self.lib.akr_hip_upload_lights(self.h, C.cast(arr, C.c_void_p), len(lights), _ptr(pw)))
 
     def build_accel(self, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0, n_threads=0,
-                    builder=0):
-        """builder: BUILDER_SAH (host binned SAH) or BUILDER_LBVH (GPU Morton / Karras)."""
-        p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder)
+                    builder=0, spatial_budget=0.0):
+        """builder: BUILDER_SAH (host binned SAH), BUILDER_LBVH (GPU Morton / Karras) or BUILDER_SBVH
+        (host SBVH with the reference's spatial splits; spatial_budget = extra references / triangles)."""
+        p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget)
         self._check(self.lib.akr_hip_build_accel(self.h, C.byref(p)))
         return self.accel_info()
 

@@ -8,6 +8,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <functional>
 #include <limits>
 #include <mutex>
@@ -72,6 +73,43 @@ struct Task {
     Box box, cbox;
 };
 
+// SBVH reference: a triangle and the part of its bounds this reference covers (spatial splits
+// clip it; bvh-accelerator.h:568-607)
+struct SRef {
+    uint32_t prim;
+    Box box;
+};
+
+struct STask {
+    uint32_t node;
+    int depth;
+    Box box;
+    std::vector<SRef> refs;
+};
+
+struct Job {
+    Task t;
+    std::shared_ptr<STask> s;  // non-null: an SBVH task
+};
+
+inline bool box_empty(const Box &b) { return !(b.lo[0] <= b.hi[0] && b.lo[1] <= b.hi[1] && b.lo[2] <= b.hi[2]); }
+inline Box box_and(const Box &a, const Box &b) {
+    Box r;
+    for (int i = 0; i < 3; i++) {
+        r.lo[i] = std::max(a.lo[i], b.lo[i]);
+        r.hi[i] = std::min(a.hi[i], b.hi[i]);
+    }
+    return r;
+}
+inline float round_down(double x) {
+    float f = (float)x;
+    return (double)f > x ? std::nextafter(f, -std::numeric_limits<float>::infinity()) : f;
+}
+inline float round_up(double x) {
+    float f = (float)x;
+    return (double)f < x ? std::nextafter(f, std::numeric_limits<float>::infinity()) : f;
+}
+
 class Builder {
   public:
     Builder(const BvhInput &in, const akr_build_params &p) : in_(in) {
@@ -81,12 +119,18 @@ class Builder {
         max_leaf_ = std::clamp(p.max_leaf_size > 0 ? p.max_leaf_size : 4, 1, AKR_LEAF_MAX);
         ct_ = p.traversal_cost > 0 ? p.traversal_cost : 1.0f;
         ci_ = p.intersect_cost > 0 ? p.intersect_cost : 4.0f;
+        sbvh_ = p.builder == AKR_BUILDER_SBVH;
+        budget_ = p.spatial_budget > 0 ? std::min(p.spatial_budget, 4.0f) : 0.5f;
     }
 
     void run(BvhOutput &out) {
         if (n_ == 0) {
             out.nodes.assign(1, empty_vroot());
             out.tris.clear();
+            return;
+        }
+        if (sbvh_) {
+            run_sbvh(out);
             return;
         }
         pbox_.resize(n_);
@@ -167,7 +211,13 @@ class Builder {
     // ---------------------------------------------------------------- task pool
     void submit(const Task &t) {
         std::lock_guard<std::mutex> g(mu_);
-        queue_.push_back(t);
+        queue_.push_back(Job{t, nullptr});
+        pending_++;
+        cv_.notify_one();
+    }
+    void submit(std::shared_ptr<STask> t) {
+        std::lock_guard<std::mutex> g(mu_);
+        queue_.push_back(Job{Task{}, std::move(t)});
         pending_++;
         cv_.notify_one();
     }
@@ -179,16 +229,17 @@ class Builder {
     }
     void worker() {
         while (true) {
-            Task t;
+            Job j;
             {
                 std::unique_lock<std::mutex> l(mu_);
                 cv_.wait(l, [&] { return !queue_.empty() || pending_ == 0; });
                 if (queue_.empty()) return;
-                t = queue_.back();
+                j = std::move(queue_.back());
                 queue_.pop_back();
             }
             try {
-                build(t);
+                if (j.s) build_sbvh(std::move(*j.s));
+                else build(j.t);
             } catch (const std::exception &e) {
                 std::lock_guard<std::mutex> g(mu_);
                 error_ = e.what();
@@ -381,6 +432,385 @@ class Builder {
             }
     }
 
+    // ---------------------------------------------------------------- SBVH
+    // The reference's SBVH (TBVHAccelerator::recursiveBuild, bvh-accelerator.h:125-475): per node
+    // the best binned object split and, above depth 40 and when the object split's children overlap
+    // by more than 1e-5 of the root area, the best spatial split (references straddling the plane
+    // are clipped into both children, TriangleHandle::split :568-607), with the reference's
+    // unsplitting test for each straddling reference.  Task-parallel; a reference budget bounds the
+    // duplication.
+    void run_sbvh(BvhOutput &out) {
+        ref_cap_ = (uint64_t)n_ + (uint64_t)((double)budget_ * n_);
+        if (ref_cap_ >= (1ull << 31)) ref_cap_ = (1ull << 31) - 1;
+        ref_.resize(ref_cap_);
+        nodes_.resize(2 * (size_t)ref_cap_ + 1);
+        next_node_ = 0;
+        refs_total_ = n_;
+        leaf_cursor_ = 0;
+        auto root = std::make_shared<STask>();
+        root->refs.resize(n_);
+        std::vector<Box> tb(threads_);
+        parallel_chunks(0, n_, [&](uint32_t b, uint32_t e, int t) {
+            tb[t].reset();
+            for (uint32_t i = b; i < e; i++) {
+                SRef &r = root->refs[i];
+                r.prim = i;
+                r.box.reset();
+                for (int k = 0; k < 3; k++) r.box.grow(vtx(i, k));
+                tb[t].grow(r.box);
+            }
+        });
+        root->box.reset();
+        for (int t = 0; t < threads_; t++) root->box.grow(tb[t]);
+        root_area_ = root->box.area();
+        root->depth = 0;
+        root->node = alloc_node();
+        const uint32_t r = root->node;
+        submit(std::move(root));
+        drain();
+        flatten(r, out);
+    }
+
+    const float *vtx(uint32_t prim, int k) const {
+        return &in_.vertices[3 * (size_t)in_.indices[3 * (size_t)prim + k]];
+    }
+
+    // Clip reference r at plane `s` of `axis` (TriangleHandle::split): the parts of the triangle on
+    // either side, intersected with r's box; crossing points rounded outward.
+    void split_ref(const SRef &r, int axis, float s, SRef &l, SRef &rr) const {
+        Box lb, rb;
+        lb.reset();
+        rb.reset();
+        for (int i = 0; i < 3; i++) {
+            const float *v0 = vtx(r.prim, i), *v1 = vtx(r.prim, (i + 1) % 3);
+            const double p0 = v0[axis], p1 = v1[axis];
+            if (p0 <= s) lb.grow(v0);
+            if (p0 >= s) rb.grow(v0);
+            if ((p0 < s && p1 > s) || (p1 < s && p0 > s)) {
+                const double t = std::max(0.0, std::min(1.0, (s - p0) / (p1 - p0)));
+                float lo[3], hi[3];
+                for (int k = 0; k < 3; k++) {
+                    const double q = (double)v0[k] + t * ((double)v1[k] - (double)v0[k]);
+                    lo[k] = round_down(q);
+                    hi[k] = round_up(q);
+                }
+                lo[axis] = hi[axis] = s;
+                lb.grow(lo); lb.grow(hi);
+                rb.grow(lo); rb.grow(hi);
+            }
+        }
+        lb.hi[axis] = std::min(lb.hi[axis], s);
+        rb.lo[axis] = std::max(rb.lo[axis], s);
+        l.prim = rr.prim = r.prim;
+        l.box = box_and(lb, r.box);
+        rr.box = box_and(rb, r.box);
+    }
+
+    void sbvh_leaf(BNode &nd, const STask &t) {
+        const uint32_t c = (uint32_t)t.refs.size();
+        const uint64_t first = leaf_cursor_.fetch_add(c);
+        if (first + c > ref_cap_) throw std::runtime_error("bvh: reference budget exceeded");
+        for (uint32_t i = 0; i < c; i++) ref_[first + i] = t.refs[i].prim;
+        nd.leaf = true;
+        nd.first = (uint32_t)first;
+        nd.count = c;
+        nd.box = t.box;
+    }
+
+    static void centroid(const Box &b, float *c) {
+        for (int k = 0; k < 3; k++) c[k] = 0.5f * b.lo[k] + 0.5f * b.hi[k];
+    }
+
+    void build_sbvh(STask t) {
+        while (true) {
+            BNode &nd = nodes_[t.node];
+            nd.box = t.box;
+            const uint32_t n = (uint32_t)t.refs.size();
+            if (n <= 1 || (t.depth >= AKR_BVH_MAX_DEPTH - 2 && n <= (uint32_t)max_leaf_)) {
+                sbvh_leaf(nd, t);
+                return;
+            }
+            if (t.depth >= AKR_BVH_MAX_DEPTH - 2) throw std::runtime_error("bvh: depth limit exceeded");
+            const int B = bins_;
+            const bool par = n >= kParBinMin && threads_ > 1;
+            const int T = par ? threads_ : 1;
+            // centroid bounds
+            Box cb;
+            {
+                std::vector<Box> tc(T);
+                auto f = [&](uint32_t b, uint32_t e, int th) {
+                    tc[th].reset();
+                    float c[3];
+                    for (uint32_t i = b; i < e; i++) {
+                        centroid(t.refs[i].box, c);
+                        tc[th].grow(c);
+                    }
+                };
+                if (par) parallel_chunks(0, n, f); else f(0, n, 0);
+                cb.reset();
+                for (auto &x : tc) cb.grow(x);
+            }
+            const double parea = t.box.area();
+            // object split: binned centroids
+            float ks[3];
+            for (int a = 0; a < 3; a++) {
+                const float ext = cb.hi[a] - cb.lo[a];
+                ks[a] = ext > 0 ? (float)B * (1.0f - 1e-6f) / ext : 0.0f;
+            }
+            auto obin = [&](const SRef &r, int a) {
+                float c[3];
+                centroid(r.box, c);
+                return std::clamp((int)((c[a] - cb.lo[a]) * ks[a]), 0, B - 1);
+            };
+            std::vector<Bin> ob((size_t)T * 3 * kMaxBins);
+            {
+                auto f = [&](uint32_t b, uint32_t e, int th) {
+                    Bin *lb = &ob[(size_t)th * 3 * kMaxBins];
+                    for (int i = 0; i < 3 * kMaxBins; i++) lb[i].reset();
+                    for (uint32_t i = b; i < e; i++)
+                        for (int a = 0; a < 3; a++) {
+                            if (!(ks[a] > 0)) continue;
+                            Bin &x = lb[a * kMaxBins + obin(t.refs[i], a)];
+                            x.n++;
+                            x.box.grow(t.refs[i].box);
+                        }
+                };
+                if (par) parallel_chunks(0, n, f); else f(0, n, 0);
+                for (int th = 1; th < T; th++)
+                    for (int i = 0; i < 3 * kMaxBins; i++) {
+                        ob[i].n += ob[(size_t)th * 3 * kMaxBins + i].n;
+                        ob[i].box.grow(ob[(size_t)th * 3 * kMaxBins + i].box);
+                    }
+            }
+            int oaxis = -1, osplit = -1;
+            double obest = std::numeric_limits<double>::infinity();
+            Box ooverlap;
+            ooverlap.reset();
+            for (int a = 0; a < 3; a++) {
+                if (!(ks[a] > 0)) continue;
+                const Bin *bn = &ob[a * kMaxBins];
+                double rarea[kMaxBins];
+                uint32_t rcnt[kMaxBins];
+                Box rbox[kMaxBins];
+                Box acc;
+                acc.reset();
+                uint32_t c = 0;
+                for (int b = B - 1; b > 0; b--) {
+                    acc.grow(bn[b].box);
+                    c += bn[b].n;
+                    rarea[b] = acc.area();
+                    rcnt[b] = c;
+                    rbox[b] = acc;
+                }
+                acc.reset();
+                c = 0;
+                for (int b = 0; b < B - 1; b++) {
+                    acc.grow(bn[b].box);
+                    c += bn[b].n;
+                    if (c == 0 || rcnt[b + 1] == 0) continue;
+                    const double cost = acc.area() * c + rarea[b + 1] * rcnt[b + 1];
+                    if (cost < obest) {
+                        obest = cost;
+                        oaxis = a;
+                        osplit = b;
+                        ooverlap = box_and(acc, rbox[b + 1]);
+                    }
+                }
+            }
+            // spatial split, like the reference: depth <= 40, object children overlapping
+            int saxis = -1;
+            float splane = 0.0f;
+            double sbest = std::numeric_limits<double>::infinity();
+            bool try_spatial = t.depth <= 40 && refs_total_.load() < ref_cap_ && parea > 0;
+            if (try_spatial && oaxis >= 0)
+                try_spatial = !box_empty(ooverlap) && ooverlap.area() / root_area_ > 1e-5;
+            if (try_spatial) {
+                struct SBin {
+                    Box box;
+                    uint32_t enter, exit;
+                };
+                std::vector<SBin> sb((size_t)T * 3 * kMaxBins);
+                float planes[3][kMaxBins];
+                bool ok[3];
+                for (int a = 0; a < 3; a++) {
+                    const double lo = t.box.lo[a], ext = (double)t.box.hi[a] - lo;
+                    ok[a] = ext > 0;
+                    for (int j = 0; j < B - 1; j++) planes[a][j] = (float)(lo + ext * (j + 1) / B);
+                }
+                auto f = [&](uint32_t b, uint32_t e, int th) {
+                    SBin *lb = &sb[(size_t)th * 3 * kMaxBins];
+                    for (int i = 0; i < 3 * kMaxBins; i++) {
+                        lb[i].box.reset();
+                        lb[i].enter = lb[i].exit = 0;
+                    }
+                    for (uint32_t i = b; i < e; i++) {
+                        const SRef &r = t.refs[i];
+                        for (int a = 0; a < 3; a++) {
+                            if (!ok[a]) continue;
+                            const float *pl = planes[a];
+                            // first / last bin the reference's box touches (bins are [p_{j-1}, p_j])
+                            int first = (int)(std::upper_bound(pl, pl + B - 1, r.box.lo[a]) - pl);
+                            int last = (int)(std::lower_bound(pl, pl + B - 1, r.box.hi[a]) - pl);
+                            if (last < first) last = first;
+                            SRef cur = r, L, R;
+                            for (int j = first; j < last; j++) {
+                                split_ref(cur, a, pl[j], L, R);
+                                if (!box_empty(L.box)) lb[a * kMaxBins + j].box.grow(L.box);
+                                cur = R;
+                            }
+                            if (!box_empty(cur.box)) lb[a * kMaxBins + last].box.grow(cur.box);
+                            lb[a * kMaxBins + first].enter++;
+                            lb[a * kMaxBins + last].exit++;
+                        }
+                    }
+                };
+                if (par) parallel_chunks(0, n, f); else f(0, n, 0);
+                for (int th = 1; th < T; th++)
+                    for (int i = 0; i < 3 * kMaxBins; i++) {
+                        const SBin &x = sb[(size_t)th * 3 * kMaxBins + i];
+                        sb[i].box.grow(x.box);
+                        sb[i].enter += x.enter;
+                        sb[i].exit += x.exit;
+                    }
+                for (int a = 0; a < 3; a++) {
+                    if (!ok[a]) continue;
+                    const SBin *bn = &sb[a * kMaxBins];
+                    double rarea[kMaxBins];
+                    uint32_t rcnt[kMaxBins];
+                    Box acc;
+                    acc.reset();
+                    uint32_t c = 0;
+                    for (int b = B - 1; b > 0; b--) {
+                        acc.grow(bn[b].box);
+                        c += bn[b].exit;
+                        rarea[b] = acc.area();
+                        rcnt[b] = c;
+                    }
+                    acc.reset();
+                    c = 0;
+                    for (int b = 0; b < B - 1; b++) {
+                        acc.grow(bn[b].box);
+                        c += bn[b].enter;
+                        if (c == 0 || rcnt[b + 1] == 0) continue;
+                        const double cost = acc.area() * c + rarea[b + 1] * rcnt[b + 1];
+                        if (cost < sbest) {
+                            sbest = cost;
+                            saxis = a;
+                            splane = planes[a][b];
+                        }
+                    }
+                }
+            }
+            const bool use_spatial = saxis >= 0 && sbest < obest;
+            const double best = use_spatial ? sbest : obest;
+            if (n <= (uint32_t)max_leaf_ &&
+                ((oaxis < 0 && saxis < 0) || ci_ * (double)n <= ct_ + ci_ * best / (parea > 0 ? parea : 1.0))) {
+                sbvh_leaf(nd, t);
+                return;
+            }
+            auto lt = std::make_shared<STask>(), rt = std::make_shared<STask>();
+            int axis = -1;
+            if (use_spatial) {
+                axis = saxis;
+                std::vector<SRef> mid;
+                Box B1, B2;
+                B1.reset();
+                B2.reset();
+                for (const SRef &r : t.refs) {
+                    if (r.box.hi[axis] <= splane) {
+                        lt->refs.push_back(r);
+                        B1.grow(r.box);
+                    } else if (r.box.lo[axis] >= splane) {
+                        rt->refs.push_back(r);
+                        B2.grow(r.box);
+                    } else {
+                        mid.push_back(r);
+                    }
+                }
+                // straddling references: split, or kept whole on one side when that is cheaper
+                // (the reference's unsplitting test); splits draw on the reference budget
+                uint64_t want = mid.size();
+                uint64_t before = refs_total_.fetch_add(want);
+                const bool may_split = before + want <= ref_cap_;
+                uint64_t added = 0;
+                for (const SRef &r : mid) {
+                    SRef L, R;
+                    split_ref(r, axis, splane, L, R);
+                    const double N1 = (double)lt->refs.size() + 1, N2 = (double)rt->refs.size() + 1;
+                    Box b1 = B1, b2 = B2;
+                    b1.grow(r.box);
+                    b2.grow(r.box);
+                    const double csplit = B1.area() * N1 + B2.area() * N2;
+                    const double c1 = b1.area() * N1 + B2.area() * (N2 - 1);
+                    const double c2 = B1.area() * (N1 - 1) + b2.area() * N2;
+                    const bool le = box_empty(L.box), re = box_empty(R.box);
+                    if (may_split && !le && !re && csplit < std::min(c1, c2)) {
+                        lt->refs.push_back(L);
+                        rt->refs.push_back(R);
+                        B1.grow(L.box);
+                        B2.grow(R.box);
+                        added++;
+                    } else if (re || (!le && c1 <= c2)) {
+                        lt->refs.push_back(r);
+                        B1 = b1;
+                    } else {
+                        rt->refs.push_back(r);
+                        B2 = b2;
+                    }
+                }
+                refs_total_.fetch_sub(want - added);
+                lt->box = B1;
+                rt->box = B2;
+            }
+            if (!use_spatial || lt->refs.empty() || rt->refs.empty()) {
+                lt->refs.clear();
+                rt->refs.clear();
+                lt->box.reset();
+                rt->box.reset();
+                if (oaxis >= 0) {
+                    axis = oaxis;
+                    for (const SRef &r : t.refs) {
+                        STask &d = obin(r, oaxis) <= osplit ? *lt : *rt;
+                        d.refs.push_back(r);
+                        d.box.grow(r.box);
+                    }
+                } else {  // centroids coincide: halve the list
+                    if (n <= (uint32_t)max_leaf_) {
+                        sbvh_leaf(nd, t);
+                        return;
+                    }
+                    int a = 0;
+                    for (int k = 1; k < 3; k++)
+                        if (t.box.hi[k] - t.box.lo[k] > t.box.hi[a] - t.box.lo[a]) a = k;
+                    axis = a;
+                    for (uint32_t i = 0; i < n; i++) {
+                        STask &d = i < n / 2 ? *lt : *rt;
+                        d.refs.push_back(t.refs[i]);
+                        d.box.grow(t.refs[i].box);
+                    }
+                }
+            }
+            if (lt->refs.empty() || rt->refs.empty()) throw std::runtime_error("bvh: empty partition");
+            std::vector<SRef>().swap(t.refs);
+            nd.leaf = false;
+            nd.axis = (uint8_t)axis;
+            nd.left = alloc_node();
+            nd.right = alloc_node();
+            lt->node = nd.left;
+            rt->node = nd.right;
+            lt->depth = rt->depth = t.depth + 1;
+            std::shared_ptr<STask> big = lt->refs.size() >= rt->refs.size() ? lt : rt;
+            std::shared_ptr<STask> small = big == lt ? rt : lt;
+            if (big->refs.size() >= kTaskMin) {
+                submit(big);
+                t = std::move(*small);
+            } else {
+                build_sbvh(std::move(*small));
+                t = std::move(*big);
+            }
+        }
+    }
+
     // ---------------------------------------------------------------- output
     uint32_t emit(uint32_t bi, BvhOutput &out, int depth, double root_area) {
         const BNode &b = nodes_[bi];
@@ -428,7 +858,7 @@ class Builder {
         out.nodes.clear();
         out.tris.clear();
         out.nodes.reserve(next_node_.load() / 2 + 2);
-        out.tris.reserve(n_);
+        out.tris.reserve(sbvh_ ? leaf_cursor_.load() : n_);
         out.nodes.push_back(empty_vroot());
         const Box &rb = nodes_[root].box;
         double ra = rb.area();
@@ -452,7 +882,13 @@ class Builder {
     std::atomic<uint32_t> next_node_{0};
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<Task> queue_;
+    std::deque<Job> queue_;
+    // SBVH state
+    bool sbvh_ = false;
+    float budget_ = 0.5f;                    // spatial splits may add up to budget_ * n references
+    uint64_t ref_cap_ = 0;
+    std::atomic<uint64_t> refs_total_{0}, leaf_cursor_{0};
+    double root_area_ = 0;
     int64_t pending_ = 0;
     std::string error_;
 };

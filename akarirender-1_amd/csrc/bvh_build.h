@@ -3,8 +3,10 @@
 // Replaces the reference's SBVH build (src/akari/kernel/bvh-accelerator.h:125-475, called from
 // BVHAccelerator::build :673-678).  Closest-hit and occlusion results do not depend on the
 // builder (up to exact ties in t), so the builder is free to target GPU traversal cost:
-// 32-bin SAH per axis (like the reference's nBuckets, :104), no spatial splits (no duplicated
-// references), leaves of at most `max_leaf_size` triangles, task-parallel over std::thread.
+// 32-bin SAH per axis (like the reference's nBuckets, :104), leaves of at most `max_leaf_size`
+// triangles, task-parallel over std::thread.  AKR_BUILDER_SAH: object splits only (no duplicated
+// references).  AKR_BUILDER_SBVH: the reference's spatial splits as well (clipped, duplicated
+// references, up to spatial_budget * n extra).
 #pragma once
 #include <stdint.h>
 #include <vector>

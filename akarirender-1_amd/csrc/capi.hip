@@ -977,7 +977,7 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         if (params) p = *params;
         BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
         if (p.builder == AKR_BUILDER_LBVH) build_lbvh_gpu(in, ctx->bvh, ctx->stream);
-        else if (p.builder == AKR_BUILDER_SAH) build_bvh(in, p, ctx->bvh);
+        else if (p.builder == AKR_BUILDER_SAH || p.builder == AKR_BUILDER_SBVH) build_bvh(in, p, ctx->bvh);
         else throw std::runtime_error("unknown builder");
         auto &b = ctx->bvh;
         build_bvh4(b.nodes, ctx->bvh4);

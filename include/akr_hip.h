@@ -129,11 +129,14 @@ typedef struct akr_build_params {
     float intersect_cost;   /* SAH cost of a triangle test (default 4: measured best for the wide
                              * traversal, where a leaf visit also pays its exact-box test) */
     int32_t n_threads;      /* 0 = hardware concurrency */
-    int32_t builder;        /* AKR_BUILDER_SAH (host binned SAH, default) or AKR_BUILDER_LBVH (GPU) */
-    int32_t _pad[2];
+    int32_t builder;        /* AKR_BUILDER_SAH (host binned SAH, default), _LBVH (GPU) or _SBVH (host) */
+    float spatial_budget;   /* SBVH: extra references allowed, as a fraction of the triangles
+                             * (0 = default 0.5) */
+    int32_t _pad;
 } akr_build_params;
 #define AKR_BUILDER_SAH 0
 #define AKR_BUILDER_LBVH 1  /* GPU Morton/Karras build: much faster, lower tree quality */
+#define AKR_BUILDER_SBVH 2  /* host SBVH: the reference's spatial splits (bvh-accelerator.h:125-475) */
 
 typedef struct akr_accel_info {
     uint64_t n_nodes;       /* 64-byte BVH2 nodes, node 0 is the virtual root */

@@ -38,8 +38,53 @@ def cornell(resolution=(64, 64)):
     return scene.cornell_scene(CORNELL_MESH, resolution=resolution)
 
 
-def small_soup(n_tris=20000, resolution=(96, 54), seed=42):
-    return scene.soup_scene(n_tris=n_tris, resolution=resolution, seed=seed)
+def small_soup(n_tris=20000, resolution=(96, 54), seed=42, r=0.01):
+    return scene.soup_scene(n_tris=n_tris, resolution=resolution, seed=seed, r=r)
+
+
+def check_sbvh(cs, nodes, tris, max_leaf, budget=0.5, samples=6):
+    """Invariants of an SBVH export (references may be clipped and duplicated): every triangle in
+    at least one leaf and at most budget * n extra records, records equal to the mesh, child boxes
+    inside their parents, and every triangle covered by the union of its leaf boxes (a barycentric
+    grid of points, in f64, each inside at least one of the triangle's leaf boxes)."""
+    n = cs.n_tris
+    g = tris["gid"].astype(np.int64)
+    assert set(g.tolist()) == set(range(n)) and len(g) <= n + int(budget * n) + 1
+    v = cs.vertices[cs.indices]
+    assert np.array_equal(tris["v0"], v[g, 0])
+    assert np.array_equal(tris["e1"], (v[g, 1] - v[g, 0]).astype(np.float32))
+    assert np.array_equal(tris["e2"], (v[g, 2] - v[g, 0]).astype(np.float32))
+    leaf_lo = np.zeros((len(g), 3), np.float64)
+    leaf_hi = np.zeros((len(g), 3), np.float64)
+    root_lo = np.array([nodes[0]["bxy0"][0], nodes[0]["bxy0"][2], nodes[0]["bz"][0]], np.float32)
+    root_hi = np.array([nodes[0]["bxy0"][1], nodes[0]["bxy0"][3], nodes[0]["bz"][1]], np.float32)
+    stack = [(int(nodes[0]["child"][0]), root_lo, root_hi, root_lo, root_hi, 1)]
+    while stack:
+        ref, lo, hi, plo, phi, depth = stack.pop()
+        assert depth <= 64 and np.all(lo >= plo) and np.all(hi <= phi)
+        if ref & 0x80000000:
+            first, cnt = (ref & 0x7FFFFFFF) >> 3, (ref & 7) + 1
+            assert cnt <= max_leaf
+            leaf_lo[first:first + cnt] = lo
+            leaf_hi[first:first + cnt] = hi
+        else:
+            nd = nodes[ref]
+            for k, (bxy, bz) in enumerate(((nd["bxy0"], nd["bz"][:2]), (nd["bxy1"], nd["bz"][2:]))):
+                clo = np.array([bxy[0], bxy[2], bz[0]], np.float32)
+                chi = np.array([bxy[1], bxy[3], bz[1]], np.float32)
+                stack.append((int(nd["child"][k]), clo, chi, lo, hi, depth + 1))
+    vd = v.astype(np.float64)
+    bary = [(a / samples, b / samples) for a in range(samples + 1) for b in range(samples + 1 - a)]
+    order = np.argsort(g, kind="stable")
+    starts = np.searchsorted(g[order], np.arange(n + 1))
+    for tri in range(n):
+        idx = order[starts[tri]:starts[tri + 1]]
+        lo, hi = leaf_lo[idx], leaf_hi[idx]
+        for a, b in bary:
+            p = (1 - a - b) * vd[tri, 0] + a * vd[tri, 1] + b * vd[tri, 2]
+            eps = 1e-12 * (1.0 + np.abs(p))   # f64 rounding of the combination, far below an f32 ulp
+            assert np.any(np.all((p >= lo - eps) & (p <= hi + eps), axis=1)), f"triangle {tri} point {a, b} not covered"
+    return len(g) - n
 
 
 def mixed_scene(resolution=(48, 48)):

@@ -250,6 +250,24 @@ def test_render_soup_bit_exact(hip_ctx_factory, exact):
         _check_render(ctx, orc, 4, 5, [(0, 0, 64, 36)], 64, 36, exact=exact)
 
 
+@pytest.mark.parametrize("mk", ["cornell", "big_soup"])
+def test_sbvh_trace_and_render_bit_exact(hip_ctx_factory, mk):
+    """The SBVH builder's clipped, duplicated references through the wide traversal: traces and
+    renders bit-exact against the oracle walking the same BVH (and hits equal to the binned-SAH
+    BVH's up to ties)."""
+    sc = cornell((48, 48)) if mk == "cornell" else small_soup(30_000, (64, 36), r=0.2)
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, sc, builder=capi.BUILDER_SBVH)
+        if mk == "big_soup":
+            assert ctx.accel_info().n_tris > cs.n_tris   # spatial splits happened
+        lo, hi = (-0.9, 0.9) if mk == "cornell" else (-1.1, 1.1)
+        rays = random_rays(20_000, 5, lo, hi)
+        for any_hit in (False, True):
+            _check_trace(ctx, orc, cs, rays, any_hit)
+        W, H = cs.camera.resolution
+        _check_render(ctx, orc, 4, 5, [(0, 0, W, H)], W, H)
+
+
 def test_render_glossy_mix_bit_exact(hip_ctx_factory):
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, mixed_scene((48, 48)))

@@ -9,7 +9,7 @@ import pytest
 import py_oracle as O
 from akari_amd import capi, scene
 from conftest import CORNELL_MESH, ROOT
-from helpers import check_bvh as _check_bvh, cornell, random_rays, small_soup
+from helpers import check_bvh as _check_bvh, check_sbvh, cornell, random_rays, small_soup
 
 
 def test_library_exports_every_declared_symbol():
@@ -106,13 +106,15 @@ def _wide_walk(wide, signs):
     return out
 
 
+@pytest.mark.parametrize("builder", ["sah", "sbvh"])
 @pytest.mark.parametrize("leaf", [1, 4])
-def test_wide_view_invariants(leaf):
+def test_wide_view_invariants(leaf, builder):
     """The 4-wide traversal view: every leaf's exact box lies inside every quantized slot box on
     its path (the wide test can only pass more often), leaf records cover the triangles once, and
     for every direction octant the leaves come in the BVH2 depth-first order."""
-    cs = scene.compile_scene(small_soup(5_000))
-    nodes, tris, info, wide = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, wide=True)
+    cs = scene.compile_scene(small_soup(5_000, r=0.01 if builder == "sah" else 0.2))
+    nodes, tris, info, wide = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, wide=True,
+                                                  builder=capi.BUILDER_SBVH if builder == "sbvh" else 0)
     wn, lv, root = wide
     assert sorted((int(l["first"]), int(l["count"])) for l in lv) == sorted(_bvh2_leaf_order(nodes, (1, 1, 1)))
     for octant in range(8):
@@ -125,11 +127,32 @@ def test_wide_view_invariants(leaf):
                     assert np.all(lo <= lv[i]["lo"]) and np.all(hi >= lv[i]["hi"])
 
 
-@pytest.mark.parametrize("mk", ["cornell", "soup"])
-def test_oracle_bvh_matches_brute_force(mk):
-    sc = cornell() if mk == "cornell" else small_soup(20_000)
+@pytest.mark.parametrize("leaf", [1, 4])
+@pytest.mark.parametrize("mk", ["cornell", "soup", "big_soup"])
+def test_sbvh_builder_invariants(mk, leaf):
+    """The SBVH builder (the reference's spatial splits, bvh-accelerator.h:125-475): clipped and
+    duplicated references within the budget, every triangle covered by its leaf boxes."""
+    sc = {"cornell": cornell, "soup": lambda: small_soup(20_000), "big_soup": lambda: small_soup(3_000, r=0.3)}[mk]()
     cs = scene.compile_scene(sc)
-    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    nodes, tris, info = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, builder=capi.BUILDER_SBVH)
+    extra = check_sbvh(cs, nodes, tris, leaf)
+    assert info.n_tris == cs.n_tris + extra
+    if mk == "big_soup":   # large overlapping triangles: spatial splits must have happened
+        assert extra > 0
+        _, _, sah = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf)
+        assert info.sah_cost < sah.sah_cost
+    nodes2, tris2, info2 = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf,
+                                               builder=capi.BUILDER_SBVH, spatial_budget=0.05)
+    assert check_sbvh(cs, nodes2, tris2, leaf, budget=0.05) <= 0.05 * cs.n_tris + 1
+
+
+@pytest.mark.parametrize("builder", ["sah", "sbvh"])
+@pytest.mark.parametrize("mk", ["cornell", "soup", "big_soup"])
+def test_oracle_bvh_matches_brute_force(mk, builder):
+    sc = {"cornell": cornell, "soup": lambda: small_soup(20_000), "big_soup": lambda: small_soup(3_000, r=0.3)}[mk]()
+    cs = scene.compile_scene(sc)
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices,
+                                         builder=capi.BUILDER_SBVH if builder == "sbvh" else capi.BUILDER_SAH)
     orc = O.OracleScene(cs, nodes, tris, capi)
     lo, hi = (-0.9, 0.9) if mk == "cornell" else (-1.1, 1.1)
     rays = random_rays(4096, 11, lo, hi)
