@@ -71,8 +71,10 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--leaf", type=int, default=4)
     ap.add_argument("--sah-isect", type=float, default=4.0, help="SAH triangle-test cost (traversal step = 1)")
-    ap.add_argument("--builder", choices=["sah", "lbvh", "sbvh"], default="sah",
+    ap.add_argument("--builder", choices=["sah", "lbvh", "sbvh"], default="sbvh",
                     help="host binned SAH, GPU LBVH, or host SBVH (the reference's spatial splits)")
+    ap.add_argument("--spatial-budget", type=float, default=0.0,
+                    help="SBVH: extra references allowed, as a fraction of the triangles (0: library default 0.5)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
@@ -116,7 +118,8 @@ def main():
     info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect,
                               n_threads=min(16, os.cpu_count() or 1),
                               builder={"sah": capi.BUILDER_SAH, "lbvh": capi.BUILDER_LBVH,
-                                       "sbvh": capi.BUILDER_SBVH}[args.builder])
+                                       "sbvh": capi.BUILDER_SBVH}[args.builder],
+                              spatial_budget=args.spatial_budget)
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)
