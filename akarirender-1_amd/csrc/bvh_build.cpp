@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -121,6 +122,7 @@ class Builder {
         ci_ = p.intersect_cost > 0 ? p.intersect_cost : 4.0f;
         sbvh_ = p.builder == AKR_BUILDER_SBVH;
         budget_ = p.spatial_budget > 0 ? std::min(p.spatial_budget, 4.0f) : 0.5f;
+        if (const char *e = std::getenv("AKR_SBVH_ALPHA")) alpha_ = std::atof(e);  // tuning knob
     }
 
     void run(BvhOutput &out) {
@@ -623,7 +625,7 @@ class Builder {
             double sbest = std::numeric_limits<double>::infinity();
             bool try_spatial = t.depth <= 40 && refs_total_.load() < ref_cap_ && parea > 0;
             if (try_spatial && oaxis >= 0)
-                try_spatial = !box_empty(ooverlap) && ooverlap.area() / root_area_ > 1e-5;
+                try_spatial = !box_empty(ooverlap) && ooverlap.area() / root_area_ > alpha_;
             if (try_spatial) {
                 struct SBin {
                     Box box;
@@ -886,6 +888,7 @@ class Builder {
     // SBVH state
     bool sbvh_ = false;
     float budget_ = 0.5f;                    // spatial splits may add up to budget_ * n references
+    double alpha_ = 1e-5;                    // spatial splits only where object children overlap more
     uint64_t ref_cap_ = 0;
     std::atomic<uint64_t> refs_total_{0}, leaf_cursor_{0};
     double root_area_ = 0;

@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--leaf", type=int, default=4)
+    ap.add_argument("--bins", type=int, default=32, help="SAH bins per axis (reference: 32)")
     ap.add_argument("--sah-isect", type=float, default=4.0, help="SAH triangle-test cost (traversal step = 1)")
     ap.add_argument("--builder", choices=["sah", "lbvh", "sbvh"], default="sbvh",
                     help="host binned SAH, GPU LBVH, or host SBVH (the reference's spatial splits)")
@@ -115,7 +116,7 @@ def main():
     cs = scene.compile_scene(sc)
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
-    info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect,
+    info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect, n_bins=args.bins,
                               n_threads=min(16, os.cpu_count() or 1),
                               builder={"sah": capi.BUILDER_SAH, "lbvh": capi.BUILDER_LBVH,
                                        "sbvh": capi.BUILDER_SBVH}[args.builder],
