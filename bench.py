@@ -84,8 +84,9 @@ def main():
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
     ap.add_argument("--lean", type=int, default=1, help="lean slot tests in the wide traversal (0: reference arithmetic)")
     ap.add_argument("--shadow-grid-pct", type=int, default=100, help="tuning: shadow-trace grid, %% of resident max")
-    ap.add_argument("--timed-stats", type=int, default=1,
-                    help="per-kernel HIP events inside the timed region (0: probe their overhead)")
+    ap.add_argument("--timed-stats", type=int, default=-1,
+                    help="HIP events inside the timed region: 2 = the dominant kernel (trace_closest) only, "
+                         "1 = every kernel, 0 = none (probe), -1 = 1 on a whole frame, 2 on a share of a split")
     ap.add_argument("--lookahead", type=int, default=1,
                     help="speculative sample lanes per pixel (1 = off, 0 = on from --slot-target, n = at most n lanes)")
     ap.add_argument("--slot-target", type=int, default=0, help="auto lookahead: path slots per render (0: library default)")
@@ -158,8 +159,10 @@ def main():
     cstats = ctx.kernel_stats()
     ctx.set_option("count_tests", 0)
     ctx.reset_stats()
-    if not args.timed_stats:
-        ctx.set_option("stats", 0)
+    # events around every launch cost nothing on a whole frame but ~6 % of an 8-way rank's step;
+    # trace_closest (the roofline kernel) is timed live either way
+    timed_stats = args.timed_stats if args.timed_stats >= 0 else (1 if split == 1 else 2)
+    ctx.set_option("stats", timed_stats)
 
     # timed region
     gathered = None
@@ -180,9 +183,14 @@ def main():
         elapsed = float(tt.item())
     kstats = ctx.kernel_stats()
     la = ctx.render_info()
-
     # sanity: every pixel of this rank got K samples
     assert int(wgt[:npix].min().item()) == K and int(wgt[:npix].max().item()) == K
+    # untimed per-kernel breakdown (events on every launch) over a few more steps
+    ctx.reset_stats()
+    ctx.set_option("stats", 1)
+    ctx.render_device(min(K, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    bstats = ctx.kernel_stats()
 
     if rank != 0:
         if world > 1:
@@ -195,7 +203,7 @@ def main():
                           "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3), "lookahead": la,
                           "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3),
                           "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
-                                      for k, v in kstats.items()},
+                                      for k, v in bstats.items()},
                           "rays_per_pixel": {"closest": counts["per_mode"]["closest"]["rays"] / max(1, npix),
                                              "shadow": counts["per_mode"]["shadow"]["rays"] / max(1, npix)}}),
               flush=True)
@@ -206,7 +214,7 @@ def main():
     cl = counts["per_mode"]["closest"]
     n_cl_launch = cstats.get("trace_closest", {}).get("launches", 0) or 1
     bytes_per_launch = (RAY_BYTES * cl["rays"] + BOX_BYTES * cl["box_tests"] + TRI_BYTES * cl["tri_tests"]) / n_cl_launch
-    kc = kstats["trace_closest"]
+    kc = kstats.get("trace_closest") or bstats["trace_closest"]   # timed region (breakdown pass if --timed-stats 0)
     avg_ms = kc["total_ms"] / kc["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     sh = counts["per_mode"]["shadow"]
@@ -261,8 +269,10 @@ def main():
                    "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
                    "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la},
         "roofline": roofline, "cpu_baseline": cpu,
+        # per-kernel averages from an untimed pass with events on every launch (the timed region
+        # times trace_closest only: events around every launch cost ~7 % at an 8-way rank)
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
-                    for k, v in kstats.items()},
+                    for k, v in bstats.items()},
         "bvh": {"nodes": info.n_nodes, "depth": info.max_depth, "build_s": round(info.build_ms / 1e3, 2)},
     }
     print(json.dumps(line), flush=True)

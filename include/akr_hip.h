@@ -175,7 +175,7 @@ int akr_hip_device_count(int *n);
 int akr_hip_create(int device, akr_hip_ctx **out);
 int akr_hip_destroy(akr_hip_ctx *ctx);
 const char *akr_hip_last_error(const akr_hip_ctx *ctx);
-/* Options: "stats" (per-kernel HIP-event timing on/off), "count_tests" (traversal counters),
+/* Options: "stats" (per-kernel HIP-event timing: 0 off, 1 every kernel, 2 trace_closest only), "count_tests" (traversal counters),
  * "exact_cull", "wide", "lean", "shadow_grid_pct", "rays_per_lane" (tuning / A-B),
  * "lookahead" (speculative sample lanes per pixel, DESIGN.md §3.7: 1 = off (default), 0 = on
  * whenever "slot_target" gives a pixel two or more lanes, 2..64 = on with at most that many lanes;

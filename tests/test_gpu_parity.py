@@ -413,3 +413,19 @@ def test_trace_small_batches_and_grazing(hip_ctx_factory):
         rays["d"] = d.astype(np.float32)
         _check_trace(ctx, orc, cs, rays, False)
         _check_trace(ctx, orc, cs, rays, True)
+
+
+def test_kernel_stats_modes(hip_ctx_factory):
+    """"stats" 1 times every kernel, 2 only trace_closest (bench.py's timed region at a split);
+    the image does not depend on it."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((32, 32)))
+        ref, _ = ctx.render(3, 5, [(0, 0, 32, 32)], 32, 32)
+        for mode, expect in ((1, {"raygen", "trace_closest", "shade", "trace_shadow", "splat"}), (2, {"trace_closest"})):
+            ctx.reset_stats()
+            ctx.set_option("stats", mode)
+            rad, _ = ctx.render(3, 5, [(0, 0, 32, 32)], 32, 32)
+            assert np.array_equal(rad, ref)
+            ks = ctx.kernel_stats()
+            assert set(ks) == expect and ks["trace_closest"]["launches"] == 15
+        ctx.set_option("stats", 0)
