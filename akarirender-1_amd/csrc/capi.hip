@@ -187,12 +187,14 @@ struct akr_hip_ctx {
     // histogram; per slot planned offset; per pass parity active list + count, accepted lanes, chain
     DBuf<uint32_t> d_commit, d_done, d_off, d_act[2], d_acc[2], d_chain[2], d_nact;
     DBuf<uint8_t> d_hist;
-    uint32_t *h_remain = nullptr;         // pinned, [2]: pixels left after the pass of that parity
+    uint32_t *h_remain = nullptr;         // mapped host memory, [2]: pixels left after the pass of that parity
+    uint32_t *d_remain_host = nullptr;    // its device address
     hipEvent_t ev_acc[2] = {nullptr, nullptr}, ev_rem[2] = {nullptr, nullptr};
     int lookahead = 1;                    // 1 = off (default), 0 = on when it adds lanes, >= 2: on, lane cap
     int64_t slot_target = 2000000;        // lookahead budget: path slots per pass
     uint64_t cur_slots = 0;               // path slots the buffers of the current render hold
     bool cur_look = false;
+    bool la_early_exit = true;            // diagnostic: false runs all spp passes
     int last_lanes = 1, last_passes = 0;
     // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
     // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
@@ -417,7 +419,11 @@ struct akr_hip_ctx {
         for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_join_main, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1],
                               &ev_acc[0], &ev_acc[1], &ev_rem[0], &ev_rem[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_remain), 2 * sizeof(uint32_t), hipHostMallocDefault));
+        // mapped, coherent: k_store_word writes the remaining-pixel count straight into it (no DMA
+        // copy whose completion the host has to trust through an event)
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_remain), 2 * sizeof(uint32_t),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_remain_host), h_remain, 0));
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
@@ -539,6 +545,12 @@ struct akr_hip_ctx {
         return N;
     }
 
+    // host waits for both internal streams (before a DMA read-back of the film)
+    void host_join() {
+        if (side) HIPCHK(hipStreamSynchronize(side));
+        if (main_st) HIPCHK(hipStreamSynchronize(main_st));
+    }
+
     // the caller's stream sees every pass of both internal streams complete
     void join_streams(hipStream_t st) {
         // one event per internal stream: re-recording a single event before the caller's stream
@@ -639,9 +651,9 @@ struct akr_hip_ctx {
             const int ps = s & 1;
             // lookahead: stop once the pass before last finished every pixel (the last pass then
             // found nothing to do); the host stays two passes ahead of the device
-            if (la && s >= 2) {
+            if (la && s >= 2 && la_early_exit) {
                 HIPCHK(hipEventSynchronize(ev_rem[ps]));
-                if (h_remain[ps] == 0) break;
+                if (reinterpret_cast<volatile uint32_t *>(h_remain)[ps] == 0) break;
             }
             last_passes++;
             uint32_t *cnt = d_counts.p + (size_t)ps * n_count_words;
@@ -709,8 +721,7 @@ struct akr_hip_ctx {
                 if (s >= 1) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ns], 0));
                 HIPCHK(hipMemsetAsync(d_nact.p + (size_t)ns * kWorkStride, 0, sizeof(uint32_t), ms));
                 timed("la_accept", ms, [&] { launch_la_accept(look(ps), (uint32_t)N, ms); });
-                HIPCHK(hipMemcpyAsync(&h_remain[ps], d_nact.p + (size_t)ns * kWorkStride, sizeof(uint32_t),
-                                      hipMemcpyDeviceToHost, ms));
+                launch_store_word(d_nact.p + (size_t)ns * kWorkStride, d_remain_host + ps, ms);
                 HIPCHK(hipEventRecord(ev_rem[ps], ms));
                 HIPCHK(hipEventRecord(ev_acc[ps], ms));
                 HIPCHK(hipStreamWaitEvent(side, ev_acc[ps], 0));
@@ -885,6 +896,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             if (value < 0 || value > (int64_t)kLookMaxLanes)
                 throw std::runtime_error("lookahead must be in [0, 64] (0 = auto, 1 = off, n = on with at most n lanes)");
             ctx->lookahead = (int)value;
+        } else if (k == "la_early_exit") {
+            ctx->la_early_exit = value != 0;
         } else if (k == "slot_target") {
             if (value < 1) throw std::runtime_error("slot_target must be >= 1");
             ctx->slot_target = value;
@@ -1104,6 +1117,7 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
                 hipStream_t st = c->stream;
                 const uint64_t N = c->render(*params, part[k].data(), (int32_t)part[k].size(), st);
                 film[k].resize(N);
+                if (N) c->host_join();  // see merge_film
                 if (N) HIPCHK(hipMemcpyAsync(film[k].data(), c->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
                 pix[k] = c->h_pixel;
@@ -1134,6 +1148,11 @@ namespace {
 void merge_film(akr_hip_ctx *ctx, uint64_t N, float *radiance, float *weight) {
     if (N == 0) return;
     hipStream_t st = ctx->stream;
+    // the render's last splat runs on the internal side stream: wait for both internal streams on
+    // the host before the copy, rather than trusting the DMA engine to honour the caller stream's
+    // cross-stream event waits (two flaky short-weight reads were seen, never reproduced)
+    ctx->host_join();
+    HIPCHK(hipStreamSynchronize(st));
     std::vector<float4> film(N);
     HIPCHK(hipMemcpyAsync(film.data(), ctx->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

@@ -12,6 +12,7 @@ int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st);
+void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st);
 void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st);
 void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st);
 void launch_la_accept(const LookArgs &a, uint32_t max_active, hipStream_t st);

@@ -1286,6 +1286,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint
     w[i] = f.w;
 }
 
+// one word from device memory into mapped host memory (the host polls it after an event)
+__global__ void k_store_word(const uint32_t *src, uint32_t *dst) {
+    if (threadIdx.x == 0) {
+        __atomic_store_n(dst, *src, __ATOMIC_RELAXED);
+        __threadfence_system();
+    }
+}
+
 // ------------------------------------------------------------------------------------ launch
 static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
@@ -1337,6 +1345,9 @@ void launch_raygen(const RaygenArgs &a, hipStream_t st) {
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_shade, dim3((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock)), dim3(kShadeBlock), 0, st, a);
+}
+void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st) {
+    hipLaunchKernelGGL(k_store_word, dim3(1), dim3(64), 0, st, src, dst);
 }
 void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st) {
     if (a.n_pix == 0) return;
