@@ -59,7 +59,7 @@ from akari_amd.dist import tiles_for_rank  # noqa: E402  (interleaved tile k -> 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", choices=["soup", "cornell"], default="soup",
                     help="soup: C3, the headline workload; cornell: C2 (BASELINE.json configs[1], the reference's "
