@@ -39,18 +39,30 @@ def test_bvh_builder_invariants(leaf):
     _check_bvh(cs, nodes, tris, leaf)
 
 
-def test_bvh_degenerate_inputs():
+@pytest.mark.parametrize("builder", [capi.BUILDER_SAH, capi.BUILDER_SBVH])
+def test_bvh_degenerate_inputs(builder):
     # identical triangles (all centroids equal) force the median split; zero-area triangles stay in
     v = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (300, 1))
     v[-3:] = [[0.5, 0.5, 0.5]] * 3
     idx = np.arange(900, dtype=np.int32).reshape(-1, 3)
-    nodes, tris, info = capi.build_bvh_host(v, idx, max_leaf_size=4)
-    assert sorted(tris["gid"].tolist()) == list(range(300))
+    nodes, tris, info = capi.build_bvh_host(v, idx, max_leaf_size=4, builder=builder)
+    assert set(tris["gid"].tolist()) == set(range(300))
+    if builder == capi.BUILDER_SAH:
+        assert sorted(tris["gid"].tolist()) == list(range(300))
     assert info.max_depth <= 64
-    n0, t0, _ = capi.build_bvh_host(np.zeros((0, 3), np.float32), np.zeros((0, 3), np.int32))
+    # a single triangle, axis-aligned (flat) triangles, a point, huge coordinates
+    for tri in ([[0, 0, 0], [1, 0, 0], [0, 1, 0]], [[0, 0, 0], [0, 0, 0], [0, 0, 0]],
+                [[-1e30, 0, 0], [1e30, 0, 0], [0, 1e30, 0]]):
+        n1, t1, _ = capi.build_bvh_host(np.array(tri, np.float32), np.array([[0, 1, 2]], np.int32), builder=builder)
+        assert t1["gid"].tolist() == [0]
+    flat = np.random.default_rng(3).uniform(-1, 1, (3000, 3)).astype(np.float32)
+    flat[:, 2] = 0.0
+    nf, tf, inf_ = capi.build_bvh_host(flat, np.arange(3000, dtype=np.int32).reshape(-1, 3), builder=builder)
+    assert set(tf["gid"].tolist()) == set(range(1000)) and inf_.max_depth <= 64
+    n0, t0, _ = capi.build_bvh_host(np.zeros((0, 3), np.float32), np.zeros((0, 3), np.int32), builder=builder)
     assert n0.shape[0] == 1 and t0.shape[0] == 0 and n0[0]["child"][0] == 0xFFFFFFFF
     with pytest.raises(capi.AkrError):
-        capi.build_bvh_host(v, np.array([[0, 1, 5000]], np.int32))
+        capi.build_bvh_host(v, np.array([[0, 1, 5000]], np.int32), builder=builder)
 
 
 def _bvh2_leaf_order(nodes, signs):
