@@ -625,6 +625,83 @@ def cornell_scene(mesh_path, resolution=(512, 512), spp=16, max_depth=5) -> Scen
     return Scene(camera=cam, shapes=[mesh], integrator=PathIntegrator(spp=spp, max_depth=max_depth, tile_size=1024))
 
 
+def _grid(o, u, v, nu, nv, normal, uv_scale, mat):
+    """A planar grid of nu x nv quads spanning o + [0,1] u + [0,1] v: (vertices [6q, 3], normals
+    [2q, 9], texcoords [2q, 6], material ids [2q]); texcoords run over [0, uv_scale]."""
+    o, u, v = (np.asarray(a, np.float64) for a in (o, u, v))
+    a, b = np.meshgrid(np.arange(nu), np.arange(nv), indexing="ij")
+    a, b = a.reshape(-1, 1), b.reshape(-1, 1)
+    p = lambda i, j: o + (i / nu) * u + (j / nv) * v
+    c00, c10, c11, c01 = p(a, b), p(a + 1, b), p(a + 1, b + 1), p(a, b + 1)
+    verts = np.stack([c00, c10, c11, c00, c11, c01], axis=1).reshape(-1, 3).astype(np.float32)
+    t = lambda i, j: np.concatenate([i / nu * uv_scale[0], j / nv * uv_scale[1]], axis=1)
+    tc = np.stack([t(a, b), t(a + 1, b), t(a + 1, b + 1), t(a, b), t(a + 1, b + 1), t(a, b + 1)], axis=1)
+    q = nu * nv
+    return (verts, np.tile(np.asarray(normal, np.float32), (2 * q, 3)), tc.reshape(-1, 6).astype(np.float32),
+            np.full(2 * q, mat, np.int32))
+
+
+def _pattern(h, w, seed, base, contrast):
+    """A procedural RGBA texture: coloured checker tiles with per-tile noise, float32 [h, w, 4]."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    check = ((x // (w // 8) + y // (h // 8)) % 2).astype(np.float32)
+    noise = rng.random((h, w)).astype(np.float32)
+    img = np.empty((h, w, 4), np.float32)
+    for c in range(3):
+        img[..., c] = np.clip(base[c] * (1 - contrast + contrast * check) * (0.85 + 0.15 * noise), 0, 1)
+    img[..., 3] = 1.0
+    return img
+
+
+def hall_scene(resolution=(3840, 2160), detail=1.0, spp=256, max_depth=5) -> Scene:
+    """Config C4 stand-in (a Sponza-class textured scene; the reference ships none):
+    a hall 20 x 8 x 8 with tessellated floor, ceiling and walls, two rows of columns, image-textured
+    Diffuse, Glossy (image roughness) and Mix (image fraction) materials, and six emissive ceiling
+    panels (area lights only: the reference has no HDRI light).  detail = 1 gives ~270K triangles."""
+    n = lambda k: max(1, int(round(k * detail)))
+    tex_floor = ImageTexture(_pattern(256, 256, 1, (0.8, 0.7, 0.55), 0.5))
+    tex_rough = ImageTexture(_pattern(64, 64, 2, (0.6, 0.6, 0.6), 0.8))
+    tex_wall = ImageTexture(_pattern(256, 256, 3, (0.75, 0.6, 0.5), 0.3))
+    tex_frac = ImageTexture(_pattern(32, 32, 4, (0.7, 0.7, 0.7), 0.9))
+    ct = ConstantTexture
+    diffuse_floor = DiffuseMaterial(tex_floor)
+    mats = [MixMaterial(tex_frac, diffuse_floor, GlossyMaterial(tex_floor, tex_rough)),   # 0 floor
+            DiffuseMaterial(tex_wall),                                                     # 1 walls
+            DiffuseMaterial(ct([0.7, 0.7, 0.68])),                                         # 2 ceiling
+            GlossyMaterial(ct([0.8, 0.75, 0.7]), ct([0.35, 0.35, 0.35])),                  # 3 columns
+            EmissiveMaterial(ct([12.0, 11.0, 9.0]))]                                       # 4 lights
+    parts = [
+        _grid((-10, 0, -4), (20, 0, 0), (0, 0, 8), n(256), n(128), (0, 1, 0), (10, 4), 0),     # floor
+        _grid((-10, 8, -4), (0, 0, 8), (20, 0, 0), n(128), n(256), (0, -1, 0), (4, 10), 2),    # ceiling
+        _grid((-10, 0, -4), (0, 8, 0), (20, 0, 0), n(64), n(256), (0, 0, 1), (3, 8), 1),       # wall z = -4
+        _grid((-10, 0, 4), (20, 0, 0), (0, 8, 0), n(256), n(64), (0, 0, -1), (8, 3), 1),       # wall z = +4
+        _grid((-10, 0, -4), (0, 0, 8), (0, 8, 0), n(128), n(128), (1, 0, 0), (3, 3), 1),      # wall x = -10
+        _grid((10, 0, -4), (0, 8, 0), (0, 0, 8), n(128), n(128), (-1, 0, 0), (3, 3), 1),      # wall x = +10
+    ]
+    for zc in (-2.5, 2.5):
+        for xc in np.arange(-8.0, 8.01, 2.0):
+            w = 0.3
+            x0, x1, z0, z1 = xc - w, xc + w, zc - w, zc + w
+            parts += [_grid((x0, 0, z1), (x1 - x0, 0, 0), (0, 8, 0), n(4), n(48), (0, 0, 1), (1, 4), 3),
+                      _grid((x1, 0, z0), (x0 - x1, 0, 0), (0, 8, 0), n(4), n(48), (0, 0, -1), (1, 4), 3),
+                      _grid((x1, 0, z1), (0, 0, z0 - z1), (0, 8, 0), n(4), n(48), (1, 0, 0), (1, 4), 3),
+                      _grid((x0, 0, z0), (0, 0, z1 - z0), (0, 8, 0), n(4), n(48), (-1, 0, 0), (1, 4), 3)]
+    for xc in (-7.0, 0.0, 7.0):
+        for zc in (-1.5, 1.5):
+            # winding u x v = -y: the panel's geometric normal faces down (one-sided AreaLight)
+            parts.append(_grid((xc - 1, 7.99, zc - 0.5), (2, 0, 0), (0, 0, 1), 1, 1, (0, -1, 0), (1, 1), 4))
+    verts = np.concatenate([p[0] for p in parts])
+    normals = np.concatenate([p[1] for p in parts])
+    tcs = np.concatenate([p[2] for p in parts])
+    mi = np.concatenate([p[3] for p in parts])
+    idx = np.arange(verts.shape[0], dtype=np.int32).reshape(-1, 3)
+    mesh = Mesh(verts, idx, normals, tcs, mi, mats)
+    cam = PerspectiveCamera(position=(-9.0, 3.0, 0.0), rotation=(-90.0, -8.0, 0.0), fov=60.0,
+                            resolution=tuple(resolution))
+    return Scene(camera=cam, shapes=[mesh], integrator=PathIntegrator(spp=spp, max_depth=max_depth))
+
+
 def soup_scene(n_tris=10_000_000, resolution=(1920, 1080), seed=42, r=0.01, spp=1024, max_depth=5) -> Scene:
     """Config C3: n_tris random triangles + a 2-triangle emissive quad."""
     v, n, t = capi.generate_soup(n_tris, seed, r)

@@ -23,6 +23,7 @@ sys.path.insert(0, str(ROOT / "akarirender-1_amd"))
 
 METRIC = "Msamples/sec (whole node), 10M-tri scene 1080p 1024spp, 1/2/4/8 MI355X"
 METRIC_CORNELL = "Msamples/sec, Cornell box 1080p 1024spp, 1x MI355X (BASELINE.json configs[1])"
+METRIC_HALL = "Msamples/sec, Sponza-class textured scene 4K (BASELINE.json configs[3] stand-in), 1x MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic bytes per ray / AABB / triangle test
 
@@ -61,12 +62,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", choices=["soup", "cornell"], default="soup",
+    ap.add_argument("--scene", choices=["soup", "cornell", "hall"], default="soup",
                     help="soup: C3, the headline workload; cornell: C2 (BASELINE.json configs[1], the reference's "
-                         "Cornell box at 1080p on one GPU; a side measurement, not the driver's line)")
+                         "Cornell box at 1080p on one GPU); hall: C4 stand-in (configs[3], a synthetic textured hall "
+                         "at 3840x2160); cornell and hall are side measurements, not the driver's line")
     ap.add_argument("--tris", type=int, default=10_000_000)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=0, help="0: 1920 (3840 for --scene hall)")
+    ap.add_argument("--height", type=int, default=0, help="0: 1080 (2160 for --scene hall)")
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--leaf", type=int, default=4)
@@ -108,10 +110,14 @@ def main():
 
     from akari_amd import capi, scene
 
-    W, H, K, Wm = args.width, args.height, args.steps, args.warmup
+    W = args.width or (3840 if args.scene == "hall" else 1920)
+    H = args.height or (2160 if args.scene == "hall" else 1080)
+    K, Wm = args.steps, args.warmup
     t0 = time.time()
     if args.scene == "cornell":
         sc = scene.cornell_scene(ROOT / "tests" / "golden" / "CornellBox-Original.obj.mesh", resolution=(W, H))
+    elif args.scene == "hall":
+        sc = scene.hall_scene(resolution=(W, H))
     else:
         sc = scene.soup_scene(n_tris=args.tris, resolution=(W, H))
     cs = scene.compile_scene(sc)
@@ -260,11 +266,13 @@ def main():
                "value_tight_cull": round(cpx * args.cpu_spp / dt_tight / 1e6, 4)}
 
     line = {
-        "metric": METRIC if args.scene == "soup" else METRIC_CORNELL, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
+        "metric": {"soup": METRIC, "cornell": METRIC_CORNELL, "hall": METRIC_HALL}[args.scene], "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
         "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "C3 synthetic triangle soup (SURVEY.md §8d)" if args.scene == "soup" else
-                   "C2 Cornell box (reference fixture CornellBox-Original.obj.mesh, SURVEY.md §8d)", "triangles": cs.n_tris,
+        "config": {"workload": {"soup": "C3 synthetic triangle soup (SURVEY.md §8d)",
+                                "cornell": "C2 Cornell box (reference fixture CornellBox-Original.obj.mesh, SURVEY.md §8d)",
+                                "hall": "C4 stand-in: synthetic textured hall, Diffuse/Glossy/Mix with image textures, "
+                                        "area lights (scene.hall_scene)"}[args.scene], "triangles": cs.n_tris,
                    "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
                    "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
                    "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la},

@@ -274,6 +274,15 @@ def test_render_glossy_mix_bit_exact(hip_ctx_factory):
         _check_render(ctx, orc, 8, 5, [(0, 0, 48, 48)], 48, 48)
 
 
+def test_render_hall_bit_exact(hip_ctx_factory):
+    """The C4 stand-in (scene.hall_scene: tessellated, image-textured Diffuse / Glossy / Mix, six
+    one-sided ceiling lights), coarse tessellation, against the oracle."""
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, scene.hall_scene((64, 36), detail=0.1), builder=capi.BUILDER_SBVH)
+        rad, w = _check_render(ctx, orc, 4, 5, [(0, 0, 64, 36)], 64, 36)
+        assert rad.mean() > 0
+
+
 def test_render_image_textures_bit_exact(hip_ctx_factory):
     """ImageTexture (texture.h:39-57, View lookup image.hpp:83-99) on diffuse colour, glossy
     roughness, mix fraction and emission, with texcoords outside [0, 1]."""
