@@ -67,16 +67,22 @@ struct ShadeTri {          // Triangle<C> data of one global triangle id (shape.
     float4 e;              // n2.xyz, 0
 };
 
+// Device copy of a texture (akr_texture + its image's size and offset): one 32-B record per
+// lookup, so an image texel is two dependent loads instead of four.
+struct TexDev {
+    int32_t type;                  // AKR_TEX_CONSTANT / AKR_TEX_IMAGE
+    float value[3];                // constant colour
+    int32_t w, h;                  // image size
+    int64_t off;                   // image's first float in SceneDev::images
+};
+
 struct SceneDev {
     const ShadeTri *tri;           // per global triangle id
     const float *texcoords;        // 6 per triangle (read only when has_image_tex)
     int32_t has_image_tex;
     const akr_material *mats;
-    const akr_texture *texs;
+    const TexDev *texs;
     const float *images;
-    const int64_t *image_off;
-    const int32_t *image_w;
-    const int32_t *image_h;
     const LightDev *lights;
     const float *light_cdf;        // n_lights + 1
     const float *light_func;       // n_lights

@@ -162,10 +162,8 @@ struct akr_hip_ctx {
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
-    DBuf<int32_t> d_img_w, d_img_h;
-    DBuf<int64_t> d_img_off;
     DBuf<akr_material> d_mats;
-    DBuf<akr_texture> d_texs;
+    DBuf<TexDev> d_texs;
     DBuf<LightDev> d_lights;
     DBuf<uint32_t> d_mesh_base;
     float func_int = 0;
@@ -299,9 +297,6 @@ struct akr_hip_ctx {
         s.mats = d_mats.p;
         s.texs = d_texs.p;
         s.images = d_images.p;
-        s.image_off = d_img_off.p;
-        s.image_w = d_img_w.p;
-        s.image_h = d_img_h.p;
         s.lights = d_lights.p;
         s.light_cdf = d_cdf.p;
         s.light_func = d_func.p;
@@ -353,11 +348,21 @@ struct akr_hip_ctx {
         d_shade_tri.upload(st.data(), st.size(), stream);
         if (has_image_tex) d_tc.upload(texcoords.data(), texcoords.size(), stream);
         d_mats.upload(mats.data(), mats.size(), stream);
-        d_texs.upload(texs.data(), texs.size(), stream);
+        std::vector<TexDev> td(texs.size());
+        for (size_t k = 0; k < texs.size(); k++) {
+            const akr_texture &t = texs[k];
+            TexDev &d = td[k];
+            std::memset(&d, 0, sizeof(d));
+            d.type = t.type;
+            for (int c = 0; c < 3; c++) d.value[c] = t.value[c];
+            if (t.type == AKR_TEX_IMAGE) {
+                d.w = img_w[t.image];
+                d.h = img_h[t.image];
+                d.off = img_off[t.image];
+            }
+        }
+        d_texs.upload(td.data(), td.size(), stream);
         d_images.upload(images.data(), images.size(), stream);
-        d_img_off.upload(img_off.data(), img_off.size(), stream);
-        d_img_w.upload(img_w.data(), img_w.size(), stream);
-        d_img_h.upload(img_h.data(), img_h.size(), stream);
         d_mesh_base.upload(mesh_base.data(), mesh_base.size(), stream);
         // lights: AreaLight records + Distribution1D over `power` (common/distribution.h:46-64)
         std::vector<LightDev> ld;

@@ -1008,15 +1008,15 @@ __global__ __launch_bounds__(kBlock) void k_la_accept(LookArgs a) {
 // ------------------------------------------------------------------------------------- shade
 // Texture::evaluate (texture.h:30-66; image lookup core/image.hpp:83-99)
 __device__ __forceinline__ V3 tex_eval(const SceneDev &s, int32_t ti, V2 tc) {
-    const akr_texture t = s.texs[ti];
+    const TexDev t = s.texs[ti];
     if (t.type == AKR_TEX_CONSTANT) return v3(t.value[0], t.value[1], t.value[2]);
     float x = fmodf(tc.x, 1.0f);
     float y = 1.0f - fmodf(tc.y, 1.0f);
-    const int w = s.image_w[t.image], h = s.image_h[t.image];
+    const int w = t.w, h = t.h;
     int ix = (int)(x * (float)w), iy = (int)(y * (float)h);
     ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
     iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
-    const float *p = s.images + s.image_off[t.image] + 4 * ((int64_t)ix + (int64_t)iy * w);
+    const float *p = s.images + t.off + 4 * ((int64_t)ix + (int64_t)iy * w);
     return v3(p[0], p[1], p[2]);
 }
 
