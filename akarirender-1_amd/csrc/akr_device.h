@@ -17,6 +17,10 @@
 namespace akr {
 
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
+#ifndef AKR_TRACE_BLOCK
+#define AKR_TRACE_BLOCK 256
+#endif
+constexpr int kTraceBlock = AKR_TRACE_BLOCK;  // threads per traversal workgroup (the LDS stack's row)
 #ifndef AKR_STACK_LDS
 #define AKR_STACK_LDS 12
 #endif

@@ -409,7 +409,7 @@ struct akr_hip_ctx {
             trace_grid[m] = (uint32_t)(n_cu * trace_blocks_per_cu(m));
             mx = std::max(mx, trace_grid[m]);
         }
-        ovf_threads = mx * kBlock;
+        ovf_threads = mx * kTraceBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_ovf_side.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_work.reserve(kTraceWords);
@@ -432,7 +432,7 @@ struct akr_hip_ctx {
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
-        const uint64_t per_block = (uint64_t)kBlock * (uint64_t)rays_per_lane;
+        const uint64_t per_block = (uint64_t)kTraceBlock * (uint64_t)rays_per_lane;
         uint64_t need = (n + per_block - 1) / per_block;
         uint64_t cap = trace_grid[mode];
         if (mode == TRACE_SHADOW) cap = std::max<uint64_t>(1, cap * (uint64_t)shadow_grid_pct / 100);

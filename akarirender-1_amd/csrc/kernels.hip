@@ -146,7 +146,7 @@ __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_
     while (sp > 0) {
         --sp;
         unsigned long long e;
-        if (sp < kStackLds) e = s_stack[sp * kBlock + tid];
+        if (sp < kStackLds) e = s_stack[sp * kTraceBlock + tid];
         else e = ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid];
         if (!(__uint_as_float((uint32_t)(e >> 32)) > lim)) return (uint32_t)e;
     }
@@ -193,7 +193,7 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
     const float tf = left_first ? t1 : t0;
     if (pn && pf) {
         const unsigned long long e = (unsigned long long)far_ref | ((unsigned long long)__float_as_uint(tf) << 32);
-        if (sp < kStackLds) s_stack[sp * kBlock + tid] = e;
+        if (sp < kStackLds) s_stack[sp * kTraceBlock + tid] = e;
         else ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid] = e;
         sp++;
     }
@@ -243,7 +243,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, co
         for (int k = 0; k < 4; k++) {
             const bool push = (rest >> pos[k]) & 1u;
             const int e = sp + (push ? (int)__popc(rest >> (pos[k] + 1u)) : 3);
-            s_stack[e * kBlock + tid] = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
+            s_stack[e * kTraceBlock + tid] = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
         }
     } else {
 #pragma unroll
@@ -251,7 +251,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, co
             if ((rest >> pos[k]) & 1u) {
                 const int e = sp + (int)__popc(rest >> (pos[k] + 1u));
                 const unsigned long long v = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
-                if (e < kStackLds) s_stack[e * kBlock + tid] = v;
+                if (e < kStackLds) s_stack[e * kTraceBlock + tid] = v;
                 else ovf[(size_t)(e - kStackLds) * ovf_threads + gtid] = v;
             }
         }
@@ -487,13 +487,13 @@ __device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t id
 #endif
 #define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
 template <int MODE, bool COUNT, bool TIGHT, bool WIDE>
-__global__ __launch_bounds__(kBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
+__global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
     constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
-    __shared__ unsigned long long s_stack_mem[kStackLds * kBlock];
+    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
-    const uint32_t gtid = blockIdx.x * kBlock + tid;
+    const uint32_t gtid = blockIdx.x * kTraceBlock + tid;
     const uint32_t n = a.count ? *a.count : a.n;
     const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
     const uint4 *nodesu = reinterpret_cast<const uint4 *>(a.nodes);
@@ -1300,11 +1300,11 @@ static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 
 template <int MODE, bool WIDE>
 static void launch_trace_mode(bool count, bool tight, const TraceArgs &a, uint32_t grid, hipStream_t st) {
     if (count) {
-        if (tight) hipLaunchKernelGGL((k_trace<MODE, true, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_trace<MODE, true, false, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
+        if (tight) hipLaunchKernelGGL((k_trace<MODE, true, true, WIDE>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_trace<MODE, true, false, WIDE>), dim3(grid), dim3(kTraceBlock), 0, st, a);
     } else {
-        if (tight) hipLaunchKernelGGL((k_trace<MODE, false, true, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_trace<MODE, false, false, WIDE>), dim3(grid), dim3(kBlock), 0, st, a);
+        if (tight) hipLaunchKernelGGL((k_trace<MODE, false, true, WIDE>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_trace<MODE, false, false, WIDE>), dim3(grid), dim3(kTraceBlock), 0, st, a);
     }
 }
 
@@ -1325,11 +1325,11 @@ int trace_blocks_per_cu(int mode) {
     int nb = 0;
     hipError_t e;
     if (mode == TRACE_CLOSEST)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true, true>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_CLOSEST, false, true, true>, kTraceBlock, 0);
     else if (mode == TRACE_ANY)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true, true>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_ANY, false, true, true>, kTraceBlock, 0);
     else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true, true>, kBlock, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<TRACE_SHADOW, false, true, true>, kTraceBlock, 0);
     if (e != hipSuccess || nb <= 0) nb = 1;
     return nb;
 }
