@@ -48,7 +48,8 @@ struct Bvh4Output {
     float max_abs = 0.0f;  // largest |frame origin| and frame step 2^e over all wide nodes (lean test bound)
 };
 
-void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out);
+// n_threads <= 0: one per hardware thread (at most 64).
+void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads = 0);
 
 // Outward 8-bit quantization of one bound (exposed for tests): the q with fmaf(q, s, origin) on
 // the correct side of `bound`, s = 2^(e - 127).

@@ -5,7 +5,10 @@
 // two BVH2 levels and fetches 64 B for four child boxes instead of 2 x 64 B.  Correctness does
 // not rest on the quantized boxes: they only have to CONTAIN the exact ones (checked here in real
 // arithmetic, which implies the device's fmaf decode), and every leaf is re-tested with its exact box.
+#include <atomic>
 #include <cmath>
+#include <exception>
+#include <thread>
 #include <cstring>
 #include <stdexcept>
 #include "bvh_build.h"
@@ -49,48 +52,96 @@ Box child_box(const akr_bvh_node &n, int c) {
     return b;
 }
 
+// Slots of the wide node for BVH2 internal node `n`: its children, with internal children
+// replaced by their two children.
+int gather_slots(const std::vector<akr_bvh_node> &in, uint32_t n2, uint32_t slot_ref2[4], Box slot_box[4],
+                 uint32_t axis[3]) {
+    const akr_bvh_node &n = in[n2];
+    for (int s = 0; s < 4; s++) slot_ref2[s] = AKR_CHILD_EMPTY;
+    axis[0] = n.axis;
+    axis[1] = axis[2] = 0;
+    for (int c = 0; c < 2; c++) {
+        const uint32_t r = n.child[c];
+        if (r == AKR_CHILD_EMPTY) continue;
+        if (r & AKR_CHILD_LEAF) {
+            slot_ref2[2 * c] = r;
+            slot_box[2 * c] = child_box(n, c);
+        } else {
+            const akr_bvh_node &m = in[r];
+            axis[1 + c] = m.axis;
+            for (int g = 0; g < 2; g++) {
+                slot_ref2[2 * c + g] = m.child[g];
+                slot_box[2 * c + g] = child_box(m, g);
+            }
+        }
+    }
+    return 0;
+}
+
+// Layout: wide nodes in depth-first preorder (a node, then its slots' subtrees in slot order) and
+// leaves in the order that walk meets them.  Both are fixed by per-subtree counts, so every subtree
+// is written at a precomputed offset and independent subtrees are collapsed on several threads;
+// the output is the same as a serial recursive walk.
 struct Collapser {
     const std::vector<akr_bvh_node> &in;
     Bvh4Output &out;
+    std::vector<uint32_t> n_nodes, n_leaves;  // per BVH2 node: wide nodes / leaves of its wide subtree
 
-    uint32_t leaf_ref(uint32_t ref2, const Box &b) {
-        akr_bvh_leaf l;
+    struct Task {
+        uint32_t n2, node_at, leaf_at;
+        int depth;
+    };
+
+    // Post-order count pass over the wide tree (iterative: SBVH trees can be deep).
+    void count(uint32_t root) {
+        n_nodes.assign(in.size(), 0);
+        n_leaves.assign(in.size(), 0);
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        uint32_t ref[4], axis[3];
+        Box box[4];
+        while (!st.empty()) {
+            auto [n2, done] = st.back();
+            st.pop_back();
+            gather_slots(in, n2, ref, box, axis);
+            if (!done) {
+                st.push_back({n2, true});
+                for (int s = 0; s < 4; s++)
+                    if (ref[s] != AKR_CHILD_EMPTY && !(ref[s] & AKR_CHILD_LEAF)) st.push_back({ref[s], false});
+                continue;
+            }
+            uint64_t nn = 1, nl = 0;
+            for (int s = 0; s < 4; s++) {
+                if (ref[s] == AKR_CHILD_EMPTY) continue;
+                if (ref[s] & AKR_CHILD_LEAF) nl++;
+                else {
+                    nn += n_nodes[ref[s]];
+                    nl += n_leaves[ref[s]];
+                }
+            }
+            if (nn >= 0xffffffffull || nl >= AKR_CHILD_LEAF) throw std::runtime_error("too many BVH leaves for the wide format");
+            n_nodes[n2] = (uint32_t)nn;
+            n_leaves[n2] = (uint32_t)nl;
+        }
+    }
+
+    void put_leaf(uint32_t at, uint32_t ref2, const Box &b) {
+        akr_bvh_leaf &l = out.leaves[at];
         for (int k = 0; k < 3; k++) {
             l.lo[k] = b.lo[k];
             l.hi[k] = b.hi[k];
         }
         l.first = akr_leaf_first(ref2);
         l.count = akr_leaf_count(ref2);
-        out.leaves.push_back(l);
-        const uint64_t idx = out.leaves.size() - 1;
-        if (idx >= AKR_CHILD_LEAF) throw std::runtime_error("too many BVH leaves for the wide format");
-        return AKR_CHILD_LEAF | (uint32_t)idx;
     }
 
-    // Wide node for BVH2 internal node `n2`, laid out in depth-first preorder.
-    uint32_t build(uint32_t n2, int depth) {
-        if (depth > out.max_depth) out.max_depth = depth;
-        const uint32_t me = (uint32_t)out.nodes.size();
-        out.nodes.emplace_back();
-        const akr_bvh_node &n = in[n2];
-        uint32_t slot_ref2[4] = {AKR_CHILD_EMPTY, AKR_CHILD_EMPTY, AKR_CHILD_EMPTY, AKR_CHILD_EMPTY};
+    // Collapse the wide subtree of `t.n2` into its slots.  Subtrees with fewer than `spawn_below`
+    // wide nodes are collapsed in place; larger ones are handed to `spawn` (when given).
+    template <class Spawn>
+    void build(const Task &t, int &max_depth, float &max_abs, uint32_t spawn_below, Spawn &&spawn) {
+        if (t.depth > max_depth) max_depth = t.depth;
+        uint32_t slot_ref2[4], axis[3];
         Box slot_box[4];
-        uint32_t axis[3] = {n.axis, 0, 0};
-        for (int c = 0; c < 2; c++) {
-            const uint32_t r = n.child[c];
-            if (r == AKR_CHILD_EMPTY) continue;
-            if (r & AKR_CHILD_LEAF) {
-                slot_ref2[2 * c] = r;
-                slot_box[2 * c] = child_box(n, c);
-            } else {
-                const akr_bvh_node &m = in[r];
-                axis[1 + c] = m.axis;
-                for (int g = 0; g < 2; g++) {
-                    slot_ref2[2 * c + g] = m.child[g];
-                    slot_box[2 * c + g] = child_box(m, g);
-                }
-            }
-        }
+        gather_slots(in, t.n2, slot_ref2, slot_box, axis);
         // quantization frame: the union of the slot boxes
         float plo[3], phi[3];
         for (int k = 0; k < 3; k++) {
@@ -128,10 +179,11 @@ struct Collapser {
             while (e < 127 && (std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k] || !real_ge(255, pow2f(e), plo[k], phi[k]))) e++;
             if (std::fmaf(255.0f, pow2f(e), plo[k]) < phi[k] || !real_ge(255, pow2f(e), plo[k], phi[k]))
                 throw std::runtime_error("BVH bounds too large to quantize");
-            out.max_abs = std::max(out.max_abs, std::max(std::fabs(plo[k]), pow2f(e)));
+            max_abs = std::max(max_abs, std::max(std::fabs(plo[k]), pow2f(e)));
             ex[k] = (uint32_t)(e + 127);
         }
         w.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | (axis[0] | axis[1] << 2 | axis[2] << 4) << 24;
+        uint32_t node_at = t.node_at + 1, leaf_at = t.leaf_at;
         for (int s = 0; s < 4; s++) {
             const uint32_t r = slot_ref2[s];
             if (r == AKR_CHILD_EMPTY) {
@@ -143,15 +195,71 @@ struct Collapser {
                 w.q[2 * k] |= quantize_lo(slot_box[s].lo[k], w.origin[k], sc) << (8 * s);
                 w.q[2 * k + 1] |= quantize_hi(slot_box[s].hi[k], w.origin[k], sc) << (8 * s);
             }
+            if (r & AKR_CHILD_LEAF) {
+                put_leaf(leaf_at, r, slot_box[s]);
+                w.child[s] = AKR_CHILD_LEAF | leaf_at++;
+            } else {
+                const Task c{r, node_at, leaf_at, t.depth + 1};
+                w.child[s] = node_at;
+                if (n_nodes[r] >= spawn_below) spawn(c);
+                else build(c, max_depth, max_abs, spawn_below, spawn);
+                node_at += n_nodes[r];
+                leaf_at += n_leaves[r];
+            }
         }
-        // children (preorder: this node first, then its slots' subtrees in slot order)
-        for (int s = 0; s < 4; s++) {
-            const uint32_t r = slot_ref2[s];
-            if (r == AKR_CHILD_EMPTY) continue;
-            w.child[s] = (r & AKR_CHILD_LEAF) ? leaf_ref(r, slot_box[s]) : build(r, depth + 1);
+        out.nodes[t.node_at] = w;
+    }
+
+    void run(uint32_t root, int threads) {
+        count(root);
+        out.nodes.resize(n_nodes[root]);
+        out.leaves.resize(n_leaves[root]);
+        const int n_threads = threads > 0 ? std::min(threads, 64) : (int)std::min(64u, std::max(1u, std::thread::hardware_concurrency()));
+        // Top of the tree on this thread: subtrees of at least `cut` wide nodes are split further,
+        // the rest become tasks (about 32 per thread) collapsed on the pool.
+        const uint32_t cut = std::max<uint32_t>(4096, n_nodes[root] / (32u * (uint32_t)n_threads));
+        std::vector<Task> tasks, top{{root, 0, 0, 1}};
+        int max_depth = 0;
+        float max_abs = 0.0f;
+        auto defer = [&](const Task &c) { top.push_back(c); };
+        auto leave = [&](const Task &c) { tasks.push_back(c); };
+        while (!top.empty()) {
+            const Task t = top.back();
+            top.pop_back();
+            if (n_nodes[t.n2] < cut && t.node_at != 0) {
+                tasks.push_back(t);
+                continue;
+            }
+            // one level here; large children go back on `top`, small ones straight to `tasks`
+            build(t, max_depth, max_abs, 1, [&](const Task &c) {
+                if (n_nodes[c.n2] >= cut) defer(c);
+                else leave(c);
+            });
         }
-        out.nodes[me] = w;
-        return me;
+        std::atomic<size_t> next{0};
+        std::vector<int> depth_of(n_threads, 0);
+        std::vector<float> abs_of(n_threads, 0.0f);
+        std::vector<std::exception_ptr> err(n_threads);
+        auto worker = [&](int w) {
+            try {
+                auto no_spawn = [](const Task &) {};
+                for (size_t i; (i = next.fetch_add(1)) < tasks.size();)
+                    build(tasks[i], depth_of[w], abs_of[w], 0xffffffffu, no_spawn);
+            } catch (...) {
+                err[w] = std::current_exception();
+            }
+        };
+        std::vector<std::thread> ts;
+        for (int w = 1; w < n_threads; w++) ts.emplace_back(worker, w);
+        worker(0);
+        for (auto &th : ts) th.join();
+        for (int w = 0; w < n_threads; w++) {
+            if (err[w]) std::rethrow_exception(err[w]);
+            max_depth = std::max(max_depth, depth_of[w]);
+            max_abs = std::max(max_abs, abs_of[w]);
+        }
+        out.max_depth = max_depth;
+        out.max_abs = max_abs;
     }
 };
 
@@ -177,7 +285,7 @@ uint32_t quantize_hi(float bound, float origin, float s) {
     return qi;
 }
 
-void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out) {
+void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads) {
     out.nodes.clear();
     out.leaves.clear();
     out.max_depth = 0;
@@ -187,10 +295,16 @@ void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out) {
     const akr_bvh_node &vroot = bvh2[0];  // virtual root: child 0 = the real root
     const uint32_t r = vroot.child[0];
     if (r == AKR_CHILD_EMPTY) return;
-    Collapser c{bvh2, out};
-    out.nodes.reserve(bvh2.size() / 2 + 1);
-    if (r & AKR_CHILD_LEAF) out.root_ref = c.leaf_ref(r, child_box(vroot, 0));
-    else out.root_ref = c.build(r, 1);
+    if (r & AKR_CHILD_LEAF) {
+        out.leaves.resize(1);
+        Collapser c{bvh2, out, {}, {}};
+        c.put_leaf(0, r, child_box(vroot, 0));
+        out.root_ref = AKR_CHILD_LEAF;
+    } else {
+        Collapser c{bvh2, out, {}, {}};
+        c.run(r, n_threads);
+        out.root_ref = 0;
+    }
 }
 
 }  // namespace akr

@@ -1000,7 +1000,7 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         else if (p.builder == AKR_BUILDER_SAH || p.builder == AKR_BUILDER_SBVH) build_bvh(in, p, ctx->bvh);
         else throw std::runtime_error("unknown builder");
         auto &b = ctx->bvh;
-        build_bvh4(b.nodes, ctx->bvh4);
+        build_bvh4(b.nodes, ctx->bvh4, p.n_threads);
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
         // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
         // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the

@@ -123,11 +123,13 @@ def main():
     cs = scene.compile_scene(sc)
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
+    t_setup = time.perf_counter()
     info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect, n_bins=args.bins,
                               n_threads=min(16, os.cpu_count() or 1),
                               builder={"sah": capi.BUILDER_SAH, "lbvh": capi.BUILDER_LBVH,
                                        "sbvh": capi.BUILDER_SBVH}[args.builder],
                               spatial_budget=args.spatial_budget)
+    t_setup = time.perf_counter() - t_setup  # BVH2 build + wide collapse + upload
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)
@@ -281,7 +283,8 @@ def main():
         # times trace_closest only: events around every launch cost ~7 % at an 8-way rank)
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                     for k, v in bstats.items()},
-        "bvh": {"nodes": info.n_nodes, "depth": info.max_depth, "build_s": round(info.build_ms / 1e3, 2)},
+        "bvh": {"nodes": info.n_nodes, "depth": info.max_depth, "build_s": round(info.build_ms / 1e3, 2),
+                "setup_s": round(t_setup, 2)},
     }
     print(json.dumps(line), flush=True)
     if world > 1:
