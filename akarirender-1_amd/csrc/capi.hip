@@ -1005,37 +1005,55 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
         // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the
         // wide nodes become float4 offsets into the blob.
-        std::vector<uint32_t> leaf_off(ctx->bvh4.leaves.size());
-        std::vector<float4> blob;
+        // Offsets by a serial prefix sum, then the records and their triangles are copied on
+        // `n_threads` threads (the blob is ~1 GB on C3).
+        const auto &leaves = ctx->bvh4.leaves;
+        std::vector<uint32_t> leaf_off(leaves.size());
         size_t words = 0;
-        for (const auto &l : ctx->bvh4.leaves) words += 2 + 3 * (size_t)l.count;
-        if (words >= AKR_CHILD_LEAF) throw std::runtime_error("BVH too large for the wide leaf blob");
-        blob.reserve(words);
-        const float4 *tri4 = reinterpret_cast<const float4 *>(b.tris.data());
-        for (size_t i = 0; i < ctx->bvh4.leaves.size(); i++) {
-            const akr_bvh_leaf &l = ctx->bvh4.leaves[i];
-            leaf_off[i] = (uint32_t)blob.size();
-            float4 h0, h1;
-            h0.x = l.lo[0], h0.y = l.lo[1], h0.z = l.lo[2], h0.w = l.hi[0];
-            uint32_t fc[2] = {l.first, l.count};
-            h1.x = l.hi[1], h1.y = l.hi[2];
-            std::memcpy(&h1.z, &fc[0], 4);
-            std::memcpy(&h1.w, &fc[1], 4);
-            blob.push_back(h0);
-            blob.push_back(h1);
-            for (uint32_t k = 0; k < 3 * l.count; k++) blob.push_back(tri4[3 * (size_t)l.first + k]);
+        for (size_t i = 0; i < leaves.size(); i++) {
+            if (words >= AKR_CHILD_LEAF) break;
+            leaf_off[i] = (uint32_t)words;
+            words += 2 + 3 * (size_t)leaves[i].count;
         }
+        if (words >= AKR_CHILD_LEAF) throw std::runtime_error("BVH too large for the wide leaf blob");
+        std::unique_ptr<float4[]> blob(new float4[std::max<size_t>(words, 1)]);
+        const float4 *tri4 = reinterpret_cast<const float4 *>(b.tris.data());
+        std::vector<akr_bvh4_node> wn = ctx->bvh4.nodes;
         auto remap = [&](uint32_t r) {
             return (r != AKR_CHILD_EMPTY && (r & AKR_CHILD_LEAF)) ? (AKR_CHILD_LEAF | leaf_off[r & 0x7FFFFFFFu]) : r;
         };
-        std::vector<akr_bvh4_node> wn = ctx->bvh4.nodes;
-        for (auto &n : wn)
-            for (auto &c : n.child) c = remap(c);
+        const int nt = p.n_threads > 0 ? std::min(p.n_threads, 64)
+                                       : (int)std::min(64u, std::max(1u, std::thread::hardware_concurrency()));
+        auto fill = [&](int t) {
+            const size_t l0 = leaves.size() * t / nt, l1 = leaves.size() * (t + 1) / nt;
+            for (size_t i = l0; i < l1; i++) {
+                const akr_bvh_leaf &l = leaves[i];
+                float4 *o = blob.get() + leaf_off[i];
+                float4 h0, h1;
+                h0.x = l.lo[0], h0.y = l.lo[1], h0.z = l.lo[2], h0.w = l.hi[0];
+                uint32_t fc[2] = {l.first, l.count};
+                h1.x = l.hi[1], h1.y = l.hi[2];
+                std::memcpy(&h1.z, &fc[0], 4);
+                std::memcpy(&h1.w, &fc[1], 4);
+                o[0] = h0;
+                o[1] = h1;
+                std::memcpy(o + 2, tri4 + 3 * (size_t)l.first, sizeof(float4) * 3 * (size_t)l.count);
+            }
+            const size_t n0 = wn.size() * t / nt, n1 = wn.size() * (t + 1) / nt;
+            for (size_t i = n0; i < n1; i++)
+                for (auto &c : wn[i].child) c = remap(c);
+        };
+        {
+            std::vector<std::thread> ts;
+            for (int t = 1; t < nt; t++) ts.emplace_back(fill, t);
+            fill(0);
+            for (auto &th : ts) th.join();
+        }
         ctx->wide_root_dev = remap(ctx->bvh4.root_ref);
         ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
         ctx->d_wleaves.reserve(1);
         ctx->d_wnodes.upload(wn.data(), wn.size(), ctx->stream);
-        ctx->d_wleaves.upload(blob.data(), blob.size(), ctx->stream);
+        ctx->d_wleaves.upload(blob.get(), words, ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));  // before the host staging vectors go away
         ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));
