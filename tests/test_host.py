@@ -139,6 +139,32 @@ def test_wide_view_invariants(leaf, builder):
                     assert np.all(lo <= lv[i]["lo"]) and np.all(hi >= lv[i]["hi"])
 
 
+@pytest.mark.parametrize("builder", ["sah", "sbvh"])
+def test_wide_view_preorder_parallel(builder):
+    """Large enough that the collapse runs subtrees on the thread pool (bvh_wide.cpp: pending
+    subtrees below 4096 wide nodes become tasks): nodes must still come in depth-first preorder,
+    leaves in the order that walk meets them, and two builds must agree byte for byte."""
+    cs = scene.compile_scene(small_soup(60_000, r=0.01 if builder == "sah" else 0.05))
+    b = capi.BUILDER_SBVH if builder == "sbvh" else capi.BUILDER_SAH
+    nodes, tris, info, (wn, lv, root) = capi.build_bvh_host(cs.vertices, cs.indices, wide=True, builder=b)
+    assert len(wn) > 3 * 4096
+    _, _, _, (wn2, lv2, root2) = capi.build_bvh_host(cs.vertices, cs.indices, wide=True, builder=b)
+    assert root == root2 == 0 and wn.tobytes() == wn2.tobytes() and lv.tobytes() == lv2.tobytes()
+    next_node, next_leaf = [0], [0]
+    stack = [root]
+    while stack:
+        ref = stack.pop()
+        if ref & 0x80000000:
+            assert ref & 0x7FFFFFFF == next_leaf[0]
+            next_leaf[0] += 1
+            continue
+        assert ref == next_node[0]
+        next_node[0] += 1
+        stack.extend(int(c) for c in reversed(wn[ref]["child"]) if int(c) != 0xFFFFFFFF)
+    assert next_node[0] == len(wn) and next_leaf[0] == len(lv)
+    assert sorted((int(l["first"]), int(l["count"])) for l in lv) == sorted(_bvh2_leaf_order(nodes, (1, 1, 1)))
+
+
 @pytest.mark.parametrize("leaf", [1, 4])
 @pytest.mark.parametrize("mk", ["cornell", "soup", "big_soup"])
 def test_sbvh_builder_invariants(mk, leaf):
