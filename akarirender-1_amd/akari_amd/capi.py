@@ -78,7 +78,7 @@ class KernelStat(C.Structure):
 class TraceCounts(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("box_tests", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("per_mode", (C.c_uint64 * 3) * 3),
-                ("lane_slots", (C.c_uint64 * 4) * 3)]
+                ("lane_slots", (C.c_uint64 * 4) * 3), ("deep_rays", C.c_uint64 * 3)]
 
 
 TEX_CONSTANT, TEX_IMAGE = 0, 1
@@ -404,7 +404,7 @@ class HipContext:
         modes = ("closest", "any", "shadow")
         per = {m: dict(rays=c.per_mode[k][0], box_tests=c.per_mode[k][1], tri_tests=c.per_mode[k][2],
                        slots_traversal=c.lane_slots[k][0], slots_busy=c.lane_slots[k][1],
-                       slots_tri=c.lane_slots[k][2], visits=c.lane_slots[k][3])
+                       slots_tri=c.lane_slots[k][2], visits=c.lane_slots[k][3], deep_rays=c.deep_rays[k])
                for k, m in enumerate(modes)}
         return dict(rays=c.rays, box_tests=c.box_tests, tri_tests=c.tri_tests, per_mode=per)
 

@@ -104,6 +104,7 @@ struct TraceCounters {             // reduced per wave, one atomic per wave
     unsigned long long rays, box, tri;
     unsigned long long slots_trav, slots_leaf, slots_tri;  // lane-iterations: traversal loop, busy in it, tri loop
     unsigned long long visits;                             // internal-node visits
+    unsigned long long deep;                               // rays whose stack went past kStackLds
 };
 
 struct TraceArgs {                 // kept small: fewer SGPRs, higher residency

@@ -192,14 +192,11 @@ class Builder {
             f(b, e, 0);
             return;
         }
-        std::vector<std::thread> ts;
         uint32_t chunk = (n + T - 1) / T;
-        for (int t = 0; t < T; t++) {
+        run_on_threads(T, [&](int t) {
             uint32_t cb = b + t * chunk, ce = std::min(e, cb + chunk);
-            if (cb >= ce) break;
-            ts.emplace_back([&, cb, ce, t] { f(cb, ce, t); });
-        }
-        for (auto &t : ts) t.join();
+            if (cb < ce) f(cb, ce, t);
+        });
     }
 
     uint32_t alloc_node() {
@@ -222,9 +219,7 @@ class Builder {
         cv_.notify_one();
     }
     void drain() {
-        std::vector<std::thread> ws;
-        for (int i = 0; i < threads_; i++) ws.emplace_back([this] { worker(); });
-        for (auto &w : ws) w.join();
+        run_on_threads(threads_, [this](int) { worker(); });
         if (!error_.empty()) throw std::runtime_error(error_);
     }
     void worker() {
@@ -410,16 +405,14 @@ class Builder {
         auto at = [&](int th) -> Bin (&)[3][kMaxBins] {
             return *reinterpret_cast<Bin(*)[3][kMaxBins]>(&local[(size_t)th * 3 * kMaxBins]);
         };
-        std::vector<std::thread> ts;
         uint32_t chunk = (n + threads_ - 1) / threads_;
         int used = 0;
-        for (int th = 0; th < threads_; th++) {
+        for (int th = 0; th < threads_; th++)
+            if (t.begin + th * chunk < t.end) used = th + 1;
+        run_on_threads(used, [&](int th) {
             uint32_t cb = t.begin + th * chunk, ce = std::min(t.end, cb + chunk);
-            if (cb >= ce) break;
-            used++;
-            ts.emplace_back([&, cb, ce, th] { work(cb, ce, at(th)); });
-        }
-        for (auto &x : ts) x.join();
+            work(cb, ce, at(th));
+        });
         for (int a = 0; a < 3; a++)
             for (int i = 0; i < bins_; i++) {
                 bins[a][i].reset();

@@ -9,11 +9,44 @@
 // references, up to spatial_budget * n extra).
 #pragma once
 #include <stdint.h>
+#include <exception>
+#include <thread>
 #include <vector>
 #include "../../include/akr_hip.h"
 #include "../../include/akr_bvh_format.h"
 
 namespace akr {
+
+// Runs f(k) for k in [0, n): k >= 1 on threads of their own, k = 0 on the calling thread.  Every
+// thread that was started is joined before this returns or rethrows (a joinable std::thread that is
+// destroyed during unwinding calls std::terminate); a share whose thread cannot be created
+// (std::system_error under thread or resource limits) runs on the calling thread instead.  The first
+// exception thrown by any f(k) is rethrown after the join.
+template <class F>
+void run_on_threads(int n, F &&f) {
+    std::vector<std::exception_ptr> err((size_t)(n > 0 ? n : 0));
+    auto call = [&](int k) {
+        try {
+            f(k);
+        } catch (...) {
+            err[(size_t)k] = std::current_exception();
+        }
+    };
+    std::vector<std::thread> ts;
+    std::vector<int> inline_k;
+    for (int k = 1; k < n; k++) {
+        try {
+            ts.emplace_back(call, k);
+        } catch (...) {
+            inline_k.push_back(k);
+        }
+    }
+    if (n > 0) call(0);
+    for (int k : inline_k) call(k);
+    for (auto &t : ts) t.join();
+    for (auto &e : err)
+        if (e) std::rethrow_exception(e);
+}
 
 struct BvhInput {
     const float *vertices;   // 3 * n_vertices

@@ -239,22 +239,12 @@ struct Collapser {
         std::atomic<size_t> next{0};
         std::vector<int> depth_of(n_threads, 0);
         std::vector<float> abs_of(n_threads, 0.0f);
-        std::vector<std::exception_ptr> err(n_threads);
-        auto worker = [&](int w) {
-            try {
-                auto no_spawn = [](const Task &) {};
-                for (size_t i; (i = next.fetch_add(1)) < tasks.size();)
-                    build(tasks[i], depth_of[w], abs_of[w], 0xffffffffu, no_spawn);
-            } catch (...) {
-                err[w] = std::current_exception();
-            }
-        };
-        std::vector<std::thread> ts;
-        for (int w = 1; w < n_threads; w++) ts.emplace_back(worker, w);
-        worker(0);
-        for (auto &th : ts) th.join();
+        run_on_threads(n_threads, [&](int w) {
+            auto no_spawn = [](const Task &) {};
+            for (size_t i; (i = next.fetch_add(1)) < tasks.size();)
+                build(tasks[i], depth_of[w], abs_of[w], 0xffffffffu, no_spawn);
+        });
         for (int w = 0; w < n_threads; w++) {
-            if (err[w]) std::rethrow_exception(err[w]);
             max_depth = std::max(max_depth, depth_of[w]);
             max_abs = std::max(max_abs, abs_of[w]);
         }

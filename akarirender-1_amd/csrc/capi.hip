@@ -127,6 +127,24 @@ CameraDev make_camera(const akr_camera &c) {
     return cam;
 }
 
+// Mapped host words written by kernels (k_store_word) are set to this by the host before the
+// store is issued.  The host never acts on a value it has not seen change from the sentinel, so a
+// stale read (a store not yet visible when the event it waited on completed, or a value left by an
+// earlier render) can only delay a decision, never make a wrong one.
+constexpr uint32_t kMappedSentinel = 0xFFFFFFFFu;
+
+// Waits (up to ~2 s) until a mapped word no longer holds the sentinel; returns the sentinel if it
+// never changes.
+uint32_t read_mapped(const volatile uint32_t *p) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (true) {
+        const uint32_t v = *p;
+        if (v != kMappedSentinel) return v;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) return kMappedSentinel;
+        std::this_thread::yield();
+    }
+}
+
 }  // namespace
 
 struct akr_hip_ctx {
@@ -134,6 +152,15 @@ struct akr_hip_ctx {
     int n_cu = 256;
     hipStream_t stream = nullptr;
     std::string err;
+    // Every trace / render of a context is ordered after the previous one, whatever streams the
+    // caller passes: they share the refill counters, the overflow stacks and the queues.
+    hipEvent_t ev_done = nullptr;
+    bool done_recorded = false;
+    // In-band check that every slot of a render's film holds exactly spp samples (option "verify",
+    // default on): device counter + mapped host word
+    bool verify = true;
+    DBuf<uint32_t> d_bad;
+    uint32_t *h_check = nullptr, *d_check_host = nullptr;
 
     // host staging (flattened over meshes)
     std::vector<float> verts;
@@ -243,6 +270,8 @@ struct akr_hip_ctx {
                              ev_acc[0], ev_acc[1], ev_rem[0], ev_rem[1]})
             if (e) (void)hipEventDestroy(e);
         if (h_remain) (void)hipHostFree(h_remain);
+        if (h_check) (void)hipHostFree(h_check);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         if (main_st) (void)hipStreamDestroy(main_st);
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
@@ -499,6 +528,7 @@ struct akr_hip_ctx {
     void trace(const float4 *rays, uint64_t n, akr_hit *hits, int any, hipStream_t st) {
         require_ready();
         if (n >= (1ull << 32)) throw std::runtime_error("too many rays in one batch");
+        serialize(st);
         HIPCHK(hipMemsetAsync(d_work.p, 0, kTraceWords * sizeof(uint32_t), st));
         TraceArgs t = trace_args(d_work.p);
         t.rays = rays;
@@ -515,6 +545,7 @@ struct akr_hip_ctx {
             timed(any ? "trace_any" : "trace_closest", st, [&] { trace_launch(mode, !exact_cull, t, n, st); });
         }
         HIPCHK(hipGetLastError());
+        mark_done(st);
     }
 
     // Pixels of the tile list (tiles in order, row-major inside a tile) into h_pixel / d_pixel;
@@ -538,6 +569,7 @@ struct akr_hip_ctx {
         cur_look = look_ok && lookahead != 1 && look_lanes((uint32_t)N, look_budget(), look_cap()) >= 2;
         cur_slots = cur_look ? std::max<uint64_t>(N, (uint64_t)look_budget() + N / 2) : N;
         if (cur_slots >= (1ull << 31)) throw std::runtime_error("lookahead slot budget too large");
+        serialize(st);
         ensure_capacity(cur_slots);  // before any upload: a reallocation drops contents
         d_counts.reserve(2 * n_count_words);
         if (N == 0) return 0;
@@ -548,6 +580,40 @@ struct akr_hip_ctx {
         HIPCHK(hipStreamWaitEvent(main_st, ev_fork, 0));
         HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
         return N;
+    }
+
+    // order `st` after the context's previous trace / render ("one context, one
+    // order"), and record the end of this one
+    void serialize(hipStream_t st) {
+        if (done_recorded) HIPCHK(hipStreamWaitEvent(st, ev_done, 0));
+    }
+    void mark_done(hipStream_t st) {
+        HIPCHK(hipEventRecord(ev_done, st));
+        done_recorded = true;
+    }
+
+    // In-band check (option "verify"): every one of the N film slots holds exactly `spp` samples.
+    // Runs on `st` after the render has been joined into it and waits for it on the host, so a
+    // render_device with the check on returns only after the film is complete.
+    void verify_weights(hipStream_t st, uint64_t N, int spp) {
+        if (!verify || N == 0) return;
+        if (!h_check) {
+            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_check), sizeof(uint32_t),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_check_host), h_check, 0));
+        }
+        d_bad.reserve(1);
+        *reinterpret_cast<volatile uint32_t *>(h_check) = kMappedSentinel;
+        HIPCHK(hipMemsetAsync(d_bad.p, 0, sizeof(uint32_t), st));
+        launch_check_weights(d_film.p, (uint32_t)N, (float)spp, d_bad.p, st);
+        launch_store_word(d_bad.p, d_check_host, st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(st));
+        const uint32_t bad = read_mapped(h_check);
+        if (bad == kMappedSentinel) throw std::runtime_error("film check: the device never reported its result");
+        if (bad != 0)
+            throw std::runtime_error("film check: " + std::to_string(bad) + " of " + std::to_string(N) +
+                                     " pixels do not hold " + std::to_string(spp) + " samples");
     }
 
     // host waits for both internal streams (before a DMA read-back of the film)
@@ -656,9 +722,11 @@ struct akr_hip_ctx {
             const int ps = s & 1;
             // lookahead: stop once the pass before last finished every pixel (the last pass then
             // found nothing to do); the host stays two passes ahead of the device
+            // (h_remain words are reset to the sentinel before each store is issued: a stale zero
+            // left by an earlier render, or a store not yet visible, can never end the render early)
             if (la && s >= 2 && la_early_exit) {
                 HIPCHK(hipEventSynchronize(ev_rem[ps]));
-                if (reinterpret_cast<volatile uint32_t *>(h_remain)[ps] == 0) break;
+                if (read_mapped(h_remain + ps) == 0) break;
             }
             last_passes++;
             uint32_t *cnt = d_counts.p + (size_t)ps * n_count_words;
@@ -726,6 +794,7 @@ struct akr_hip_ctx {
                 if (s >= 1) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ns], 0));
                 HIPCHK(hipMemsetAsync(d_nact.p + (size_t)ns * kWorkStride, 0, sizeof(uint32_t), ms));
                 timed("la_accept", ms, [&] { launch_la_accept(look(ps), (uint32_t)N, ms); });
+                reinterpret_cast<volatile uint32_t *>(h_remain)[ps] = kMappedSentinel;
                 launch_store_word(d_nact.p + (size_t)ns * kWorkStride, d_remain_host + ps, ms);
                 HIPCHK(hipEventRecord(ev_rem[ps], ms));
                 HIPCHK(hipEventRecord(ev_acc[ps], ms));
@@ -864,6 +933,7 @@ int akr_hip_create(int device, akr_hip_ctx **out) {
     ctx->device = device;
     if (hipSetDevice(device) != hipSuccess) return -1;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return -1;
+    if (hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming) != hipSuccess) return -1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->n_cu = prop.multiProcessorCount;
@@ -901,6 +971,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             if (value < 0 || value > (int64_t)kLookMaxLanes)
                 throw std::runtime_error("lookahead must be in [0, 64] (0 = auto, 1 = off, n = on with at most n lanes)");
             ctx->lookahead = (int)value;
+        } else if (k == "verify") {
+            ctx->verify = value != 0;
         } else if (k == "la_early_exit") {
             ctx->la_early_exit = value != 0;
         } else if (k == "slot_target") {
@@ -1043,12 +1115,7 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
             for (size_t i = n0; i < n1; i++)
                 for (auto &c : wn[i].child) c = remap(c);
         };
-        {
-            std::vector<std::thread> ts;
-            for (int t = 1; t < nt; t++) ts.emplace_back(fill, t);
-            fill(0);
-            for (auto &th : ts) th.join();
-        }
+        run_on_threads(nt, fill);
         ctx->wide_root_dev = remap(ctx->bvh4.root_ref);
         ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
         ctx->d_wleaves.reserve(1);
@@ -1132,22 +1199,20 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
     std::vector<std::vector<float4>> film(n_ctx);
     std::vector<std::vector<uint32_t>> pix(n_ctx);
     std::vector<int> status(n_ctx, 0);
-    std::vector<std::thread> th;
-    for (int32_t k = 0; k < n_ctx; k++) {
-        th.emplace_back([&, k] {
-            akr_hip_ctx *c = ctxs[k];
-            status[k] = guard(c, [&] {
-                hipStream_t st = c->stream;
-                const uint64_t N = c->render(*params, part[k].data(), (int32_t)part[k].size(), st);
-                film[k].resize(N);
-                if (N) c->host_join();  // see merge_film
-                if (N) HIPCHK(hipMemcpyAsync(film[k].data(), c->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
-                HIPCHK(hipStreamSynchronize(st));
-                pix[k] = c->h_pixel;
-            });
+    run_on_threads(n_ctx, [&](int k) {
+        akr_hip_ctx *c = ctxs[k];
+        status[k] = guard(c, [&] {
+            hipStream_t st = c->stream;
+            const uint64_t N = c->render(*params, part[k].data(), (int32_t)part[k].size(), st);
+            film[k].resize(N);
+            if (N) c->host_join();  // see merge_film
+            c->verify_weights(st, N, params->spp);
+            if (N) HIPCHK(hipMemcpyAsync(film[k].data(), c->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
+            c->mark_done(st);
+            HIPCHK(hipStreamSynchronize(st));
+            pix[k] = c->h_pixel;
         });
-    }
-    for (auto &t : th) t.join();
+    });
     for (int32_t k = 0; k < n_ctx; k++)
         if (status[k] != 0) {
             if (k) lead->err = "context " + std::to_string(k) + ": " + ctxs[k]->err;
@@ -1168,17 +1233,28 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
 
 namespace {
 // Film::merge_tile (core/film.h:85-95) of the context's packed film into full-frame host buffers
-void merge_film(akr_hip_ctx *ctx, uint64_t N, float *radiance, float *weight) {
-    if (N == 0) return;
+void merge_film(akr_hip_ctx *ctx, uint64_t N, int spp, float *radiance, float *weight) {
     hipStream_t st = ctx->stream;
+    if (N == 0) {
+        ctx->mark_done(st);
+        return;
+    }
     // the render's last splat runs on the internal side stream: wait for both internal streams on
     // the host before the copy, rather than trusting the DMA engine to honour the caller stream's
     // cross-stream event waits (two flaky short-weight reads were seen, never reproduced)
     ctx->host_join();
     HIPCHK(hipStreamSynchronize(st));
+    ctx->verify_weights(st, N, spp);
     std::vector<float4> film(N);
     HIPCHK(hipMemcpyAsync(film.data(), ctx->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
+    ctx->mark_done(st);
     HIPCHK(hipStreamSynchronize(st));
+    if (ctx->verify) {  // the read-back itself: every copied slot holds spp samples
+        uint64_t bad = 0;
+        for (uint64_t k = 0; k < N; k++) bad += film[k].w != (float)spp;
+        if (bad) throw std::runtime_error("film read-back: " + std::to_string(bad) + " of " + std::to_string(N) +
+                                          " pixels do not hold " + std::to_string(spp) + " samples");
+    }
     const int W = ctx->cam.width;
     for (uint64_t k = 0; k < N; k++) {
         uint32_t px = ctx->h_pixel[k];
@@ -1195,7 +1271,7 @@ int akr_hip_render(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect
                    float *radiance, float *weight) {
     return guard(ctx, [&] {
         if (!params || !radiance || !weight) throw std::runtime_error("null argument");
-        merge_film(ctx, ctx->render(*params, tiles, n_tiles, ctx->stream), radiance, weight);
+        merge_film(ctx, ctx->render(*params, tiles, n_tiles, ctx->stream), params->spp, radiance, weight);
     });
 }
 
@@ -1203,7 +1279,7 @@ int akr_hip_render_ao(akr_hip_ctx *ctx, const akr_ao_params *params, const akr_r
                       float *radiance, float *weight) {
     return guard(ctx, [&] {
         if (!params || !radiance || !weight) throw std::runtime_error("null argument");
-        merge_film(ctx, ctx->render_ao(*params, tiles, n_tiles, ctx->stream), radiance, weight);
+        merge_film(ctx, ctx->render_ao(*params, tiles, n_tiles, ctx->stream), params->spp, radiance, weight);
     });
 }
 
@@ -1216,6 +1292,8 @@ int akr_hip_render_device(akr_hip_ctx *ctx, const akr_pt_params *params, const a
         if (n_pixels) *n_pixels = N;
         ctx->timed("unpack", st, [&] { launch_unpack(ctx->d_film.p, (uint32_t)N, d_radiance, d_weight, st); });
         HIPCHK(hipGetLastError());
+        ctx->verify_weights(st, N, params->spp);
+        ctx->mark_done(st);
     });
 }
 
@@ -1223,6 +1301,7 @@ struct akr_bvh_host {
     BvhOutput out;
     Bvh4Output wide;
     bool wide_built = false;
+    int n_threads = 0;  // the build's thread count, used by the wide collapse too
 };
 
 int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t *indices, uint64_t n_triangles,
@@ -1239,6 +1318,7 @@ int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t
         p.intersect_cost = 4.0f;
         if (params) p = *params;
         std::unique_ptr<akr_bvh_host> h(new akr_bvh_host());
+        h->n_threads = p.n_threads;
         BvhInput in{vertices, indices, n_triangles};
         build_bvh(in, p, h->out);
         if (info) {
@@ -1263,7 +1343,7 @@ int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, ui
     if (!h) return -1;
     try {
         if (!h->wide_built) {
-            build_bvh4(h->out.nodes, h->wide);
+            build_bvh4(h->out.nodes, h->wide, h->n_threads);
             h->wide_built = true;
         }
         if (n_nodes) *n_nodes = h->wide.nodes.size();
@@ -1327,6 +1407,7 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
             out->lane_slots[m][1] = c[m].slots_leaf;
             out->lane_slots[m][2] = c[m].slots_tri;
             out->lane_slots[m][3] = c[m].visits;
+            out->deep_rays[m] = c[m].deep;
         }
     });
 }

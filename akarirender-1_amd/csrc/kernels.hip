@@ -501,7 +501,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const uint32_t root = WIDE ? a.wide_root : nodesu[3].x;
     const float4 *wn = a.wide_nodes;
-    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0, c_visit = 0;
+    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0, c_visit = 0, c_deep = 0;
+    bool deep = false;  // COUNT only: this lane's ray has pushed past the LDS stack
 
     V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
     float tmin = 0.0f, tmax = 0.0f, tmaxp = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
@@ -584,6 +585,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                     if (COUNT) {
                         c_box += nt;
                         c_visit++;
+                        deep = deep || sp > kStackLds;
                     }
                 } else if (!WIDE && busy && is_internal(cur)) {
                     if (COUNT) {
@@ -596,6 +598,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                     else
                         visit_node<TIGHT, false, ANY>(nodesf, nodesu, cur, o, d, invd, tmin, tmax, best, s_stack,
                                                       stack_ovf, a.ovf_threads, tid, gtid, sp);
+                    if (COUNT) deep = deep || sp > kStackLds;
                 }
                 if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
                     leaf = cur;  // postpone the leaf and keep descending
@@ -661,6 +664,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                 busy = false;
                 emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
                 if (COUNT && a.ray_steps) a.ray_steps[idx] = steps;
+                if (COUNT) c_deep += deep ? 1 : 0;
             }
         }
         if (fresh) {
@@ -694,7 +698,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             occluded = false;
             sp = 0;
             leaf = AKR_CHILD_EMPTY;
-            if (COUNT) { c_rays++; c_box++; steps = 0; }
+            if (COUNT) { c_rays++; c_box++; steps = 0; deep = false; }
             const float tr = box_test<TIGHT, WIDE>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
             cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
             busy = true;
@@ -708,6 +712,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
         c_sleaf = wave_sum(c_sleaf);
         c_stri = wave_sum(c_stri);
         c_visit = wave_sum(c_visit);
+        c_deep = wave_sum(c_deep);
         if (__lane_id() == 0) {
             atomicAdd(&a.counters[MODE].rays, c_rays);
             atomicAdd(&a.counters[MODE].box, c_box);
@@ -716,6 +721,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             atomicAdd(&a.counters[MODE].slots_leaf, c_sleaf);
             atomicAdd(&a.counters[MODE].slots_tri, c_stri);
             atomicAdd(&a.counters[MODE].visits, c_visit);
+            atomicAdd(&a.counters[MODE].deep, c_deep);
         }
     }
 }
@@ -1286,6 +1292,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint
     w[i] = f.w;
 }
 
+// In-band read-back check: counts the film slots whose sample weight is not `expect` (one atomic
+// per wave); a render that lost samples, or a film read before its last splat, cannot pass.
+__global__ __launch_bounds__(kBlock) void k_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const unsigned long long m = __ballot(i < n && film[i].w != expect);
+    if (__lane_id() == 0 && m) atomicAdd(bad, (uint32_t)__popcll(m));
+}
+
 // one word from device memory into mapped host memory (the host polls it after an event)
 __global__ void k_store_word(const uint32_t *src, uint32_t *dst) {
     if (threadIdx.x == 0) {
@@ -1372,6 +1386,10 @@ void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t s
 void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_splat, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+}
+void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_check_weights, dim3(blocks_for(n)), dim3(kBlock), 0, st, film, n, expect, bad);
 }
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
     if (n == 0) return;

@@ -5,13 +5,18 @@ A step is one sample per pixel over the whole frame (2,073,600 path samples).  K
 render(spp=K) call per rank over that rank's tiles; the frame-end gather to rank 0 (RCCL via
 torch.distributed) is inside the timed region.  value = W*H*K / max-over-ranks time.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W].  Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank and --gpus must equal the world size.  Without it, --gpus N > 1 starts the N
+ranks itself (a torch.distributed.run child, before anything touches the GPU) and fails loudly when
+fewer than N devices are visible.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -57,9 +62,97 @@ def measured_traffic(kernel, workload):
 from akari_amd.dist import tiles_for_rank  # noqa: E402  (interleaved tile k -> rank k % world)
 
 
+def host_cpus() -> dict:
+    """The host's CPUs as the CPU baseline sees them: `nproc` (the affinity mask), os.cpu_count()
+    (every online CPU, what std::thread::hardware_concurrency() reports), the cgroup CPU quota when
+    one caps the job, and lscpu's model name.  `usable` = the CPUs this job can actually run on."""
+    info = {"nproc": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count() or 1}
+    usable = info["nproc"]
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            info["cgroup_cpus"] = round(int(quota) / int(period), 2)
+            usable = max(1, min(usable, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                info["model"] = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    info["usable"] = usable
+    return info
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_plan(gpus: int, env) -> tuple:
+    """How this invocation runs: ("spawn", N) starts N ranks under torch.distributed.run;
+    ("rank", world) runs as one rank of an already launched world (WORLD_SIZE in the environment,
+    or a single process).  --gpus 0 means "whatever the launcher gave" (1 without one); a --gpus that
+    contradicts a launcher's world size is an error, never a silently mislabelled line."""
+    env_world = env.get("WORLD_SIZE")
+    if env_world is None:
+        if gpus > 1:
+            return ("spawn", gpus)
+        return ("rank", 1)
+    world = int(env_world)
+    if gpus and gpus != world:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return ("rank", world)
+
+
+def spawn_ranks(n: int, argv, need_devices: bool = True) -> int:
+    """Start n ranks of this script as a torch.distributed.run child (one process per GPU, RCCL
+    over 127.0.0.1 rendezvous) and return its exit code.  Only counts devices first
+    (torch.cuda.device_count does not initialise the GPU), so no HIP state exists in this process."""
+    if need_devices:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()), *argv]
+    log("[launcher] " + " ".join(cmd))
+    return subprocess.run(cmd).returncode
+
+
+def launch_check(world: int, rank: int):
+    """--launch-check: the rank plumbing without a GPU (gloo): every rank joins the group and
+    all-gathers a packed film the size of its tile share; rank 0 prints the live world size."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world and dist.get_rank() == rank
+    film = torch.full((4 * 16,), float(rank))
+    gathered = torch.empty(world * film.numel())
+    if world > 1:
+        dist.all_gather_into_tensor(gathered, film)
+    else:
+        gathered.copy_(film)
+    ranks = sorted({int(v) for v in gathered.tolist()})
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_gathered": ranks}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="ranks, one per GPU (0: the launcher's WORLD_SIZE, or 1); > 1 without a launcher "
+                         "starts the ranks itself")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test the rank launch and the frame-end gather on CPU (gloo), no GPU work")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", choices=["soup", "cornell", "hall"], default="soup",
@@ -79,7 +172,9 @@ def main():
     ap.add_argument("--spatial-budget", type=float, default=0.0,
                     help="SBVH: extra references allowed, as a fraction of the triangles (0: library default 0.5)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline workers (0: the host's hardware concurrency as this job sees it, "
+                         "the reference's std::thread::hardware_concurrency(), core/parallel.cpp:32)")
     ap.add_argument("--cpu-frac", type=int, default=4, help="CPU sample = every n-th tile of the frame")
     ap.add_argument("--cpu-spp", type=int, default=1)
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
@@ -97,15 +192,24 @@ def main():
                          "(prints the per-rank time; not a bench line for the driver)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    how, world = launch_plan(args.gpus, os.environ)
+    if how == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:], need_devices=not args.launch_check))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        launch_check(world, rank)
+        return
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        live = dist.get_world_size()   # n_gpus is the live group's size, never a flag
+        if live != world:
+            raise SystemExit(f"bench.py: launched for {world} ranks, process group has {live}")
+        world = live
     dev = torch.device("cuda", local)
 
     from akari_amd import capi, scene
@@ -253,7 +357,8 @@ def main():
         orc = py_oracle.OracleScene(cs, nodes, tris, capi)
         ctiles = tiles_for_rank(W, H, args.tile, 0, args.cpu_frac)
         cpx = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in ctiles)
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        host = host_cpus()
+        threads = args.cpu_threads or host["usable"]
         # the reference CPU path's traversal (exact intersectAABB), and the same port with the tight cull
         tc = time.perf_counter()
         orc.render(args.cpu_spp, args.max_depth, tiles=ctiles, n_threads=threads, exact_cull=True)
@@ -262,7 +367,7 @@ def main():
         orc.render(args.cpu_spp, args.max_depth, tiles=ctiles, n_threads=threads, exact_cull=False)
         dt_tight = time.perf_counter() - tc
         cpu = {"value": round(cpx * args.cpu_spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-               "kind": "port",
+               "kind": "port", "host": host,
                "sample": f"every {args.cpu_frac}th {args.tile}x{args.tile} tile of the same frame ({cpx} px) x "
                          f"{args.cpu_spp} spp, same scene and BVH, reference intersectAABB, {dt:.1f} s",
                "value_tight_cull": round(cpx * args.cpu_spp / dt_tight / 1e6, 4)}

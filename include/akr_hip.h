@@ -167,6 +167,9 @@ typedef struct akr_trace_counts {
      * lanes holding a ray, triangle-loop lane-iterations, node visits]; visits / slots[0] and
      * tri_tests / slots[2] are lane utilisations. */
     uint64_t lane_slots[3][4];
+    /* rays per mode whose traversal stack grew past the LDS-resident entries into the global
+     * overflow area (the deep-stack path, kernels.hip stack_pop / wide_order_push) */
+    uint64_t deep_rays[3];
 } akr_trace_counts;
 
 int akr_hip_api_version(void);

@@ -665,6 +665,39 @@ std::vector<Work> split_work(const akr_rect *tiles, int n_tiles, int W, int H) {
     return work;
 }
 
+// Per-work-tile results (rgb sum, weight per pixel) merged into the frame after the parallel loop,
+// serially in work order.  The reference merges each finished tile under a mutex
+// (cpu/integrator.cpp:138-140, Film::merge_tile film.h:85-95); merging in a fixed order also keeps
+// overlapping tiles deterministic.  (An unlocked += from the worker threads lost updates where tiles
+// overlap: the flaky short weights of earlier parity runs.)
+struct TileFilm {
+    std::vector<size_t> off;   // first pixel of each work tile
+    std::vector<float> px;     // 4 floats per pixel: rgb sum, weight
+    explicit TileFilm(const std::vector<Work> &work) {
+        off.resize(work.size() + 1, 0);
+        for (size_t i = 0; i < work.size(); i++)
+            off[i + 1] = off[i] + (size_t)(work[i].x1 - work[i].x0) * (size_t)(work[i].y1 - work[i].y0);
+        px.assign(4 * off.back(), 0.0f);
+    }
+    float *at(size_t wi, const Work &w, int x, int y) {
+        return &px[4 * (off[wi] + (size_t)(y - w.y0) * (size_t)(w.x1 - w.x0) + (size_t)(x - w.x0))];
+    }
+    void merge(const std::vector<Work> &work, int W, float *radiance, float *weight) {
+        for (size_t wi = 0; wi < work.size(); wi++) {
+            const Work &w = work[wi];
+            for (int y = w.y0; y < w.y1; y++)
+                for (int x = w.x0; x < w.x1; x++) {
+                    const float *v = at(wi, w, x, y);
+                    const int64_t pix = (int64_t)x + (int64_t)y * W;
+                    radiance[3 * pix + 0] += v[0];
+                    radiance[3 * pix + 1] += v[1];
+                    radiance[3 * pix + 2] += v[2];
+                    weight[pix] += v[3];
+                }
+        }
+    }
+};
+
 // cpu::AmbientOcclusion::render's Li (kernel/integrators/cpu/integrator.cpp:43-60).  The camera
 // sample is generate_ray(sampler.next2d(), sampler.next2d(), p) (:76-77): C++ leaves the order of
 // the two argument evaluations unspecified; we take them left to right (lens draw first, film draw
@@ -796,6 +829,7 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
     std::vector<PathStats> pst(T);
     const float clampv = p->ray_clamp;
     const bool tight = !(p->flags & AKR_PT_EXACT_CULL);
+    TileFilm tf(work);
     parallel_for(work.size(), T, 1, [&](uint64_t wi, int tid) {
         const Work &w = work[wi];
         for (int y = w.y0; y < w.y1; y++)
@@ -815,13 +849,14 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
                     acc = add(acc, L);  // Tile::add_sample, film.h:66-70
                     wsum += 1.0f;
                 }
-                int64_t pix = (int64_t)x + (int64_t)y * W;
-                radiance[3 * pix + 0] += acc.x;  // Film::merge_tile, film.h:85-95
-                radiance[3 * pix + 1] += acc.y;
-                radiance[3 * pix + 2] += acc.z;
-                weight[pix] += wsum;
+                float *o = tf.at(wi, w, x, y);
+                o[0] = acc.x;
+                o[1] = acc.y;
+                o[2] = acc.z;
+                o[3] = wsum;
             }
     });
+    tf.merge(work, W, radiance, weight);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         for (auto &q : pst) {
@@ -845,6 +880,7 @@ int orc_render_ao(const orc_scene *s, const akr_ao_params *p, const akr_rect *ti
     int T = hw_threads(n_threads);
     std::vector<PathStats> pst(T);
     const bool tight = !(p->flags & AKR_PT_EXACT_CULL);
+    TileFilm tf(work);
     parallel_for(work.size(), T, 1, [&](uint64_t wi, int tid) {
         const Work &w = work[wi];
         for (int y = w.y0; y < w.y1; y++)
@@ -855,13 +891,12 @@ int orc_render_ao(const orc_scene *s, const akr_ao_params *p, const akr_rect *ti
                     acc += trace_ao(sc, sampler, x, y, p->occlude, tight, pst[tid]);  // Spectrum(L) per channel
                     wsum += 1.0f;
                 }
-                int64_t pix = (int64_t)x + (int64_t)y * W;
-                radiance[3 * pix + 0] += acc;  // Film::merge_tile, film.h:85-95
-                radiance[3 * pix + 1] += acc;
-                radiance[3 * pix + 2] += acc;
-                weight[pix] += wsum;
+                float *o = tf.at(wi, w, x, y);
+                o[0] = o[1] = o[2] = acc;  // Spectrum(L) per channel
+                o[3] = wsum;
             }
     });
+    tf.merge(work, W, radiance, weight);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         for (auto &q : pst) {

@@ -155,3 +155,33 @@ def check_bvh(cs, nodes, tris, max_leaf):
             stack.append((int(nd["child"][0]), nd["bxy0"], nd["bz"][:2], depth + 1))
             stack.append((int(nd["child"][1]), nd["bxy1"], nd["bz"][2:], depth + 1))
     assert seen == n
+
+
+# ref.png blocks where the reference's image was made by a different estimator: the
+# ceiling strip in the 1-cm gap above the one-sided light (y 1.98 vs ceiling 1.99), block row 2.
+REFPNG_LIGHT_GAP = [(2, c) for c in range(11, 21)]
+
+
+def refpng_ztest(rad, w, golden):
+    """Per-block z statistic of the grey level (channel mean of the sRGB8 image, 16x16 blocks)
+    against the reference's ref.png, z = (ours - ref) / sqrt((var_ours + var_ref) / 256), each
+    variance the image's own within-block pixel variance (per-block z-test; spatial
+    variation inside a block only inflates sigma).  Returns z [32, 32]."""
+    from akari_amd import film
+    grey = film.to_srgb8(rad, w).astype(np.float64).mean(axis=2).reshape(32, 16, 32, 16)
+    mo, vo = grey.mean(axis=(1, 3)), grey.var(axis=(1, 3), ddof=1)
+    mr, vr = np.asarray(golden["grey_mean"]), np.asarray(golden["grey_var"])
+    return (mo - mr) / np.sqrt((vo + vr) / 256.0 + 1e-12)
+
+
+def refpng_verdict(z):
+    """(fraction of blocks outside the light gap with |z| <= 3, failing blocks outside the gap,
+    gap blocks where ref.png is brighter by more than 3 sigma)."""
+    gap = np.zeros(z.shape, bool)
+    for r, c in REFPNG_LIGHT_GAP:
+        gap[r, c] = True
+    ok = np.abs(z) <= 3
+    outside = ~gap
+    fails = [(int(r), int(c), round(float(z[r, c]), 1)) for r, c in np.argwhere(outside & ~ok)]
+    gap_darker = int(np.count_nonzero(gap & (z < -3)))
+    return ok[outside].mean(), fails, gap_darker

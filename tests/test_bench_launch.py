@@ -1,0 +1,49 @@
+"""bench.py's rank launch: --gpus N without a launcher starts N ranks under
+torch.distributed.run; under a launcher --gpus must equal WORLD_SIZE; the JSON line's n_gpus is the
+live group's size.  Rehearsed on CPU with gloo (--launch-check: rank plumbing + frame-end gather)."""
+import json
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+
+def test_launch_plan():
+    assert bench.launch_plan(0, {}) == ("rank", 1)
+    assert bench.launch_plan(1, {}) == ("rank", 1)
+    assert bench.launch_plan(4, {}) == ("spawn", 4)
+    assert bench.launch_plan(0, {"WORLD_SIZE": "8"}) == ("rank", 8)
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}) == ("rank", 8)
+    with pytest.raises(SystemExit):
+        bench.launch_plan(2, {"WORLD_SIZE": "1"})
+    with pytest.raises(SystemExit):
+        bench.launch_plan(8, {"WORLD_SIZE": "2"})
+
+
+def _run(args, timeout=240):
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=str(ROOT))
+
+
+def test_gpus_2_spawns_two_gloo_ranks():
+    r = _run(["--gpus", "2", "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_gathered"] == [0, 1]
+
+
+def test_gpus_beyond_visible_devices_fails_loudly():
+    # this container has no GPU: asking for 2 ranks of real work must fail before any rank starts
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two or more devices visible")
+    r = _run(["--gpus", "2", "--steps", "1"], timeout=120)
+    assert r.returncode != 0
+    assert "needs 2 visible GPUs" in r.stderr

@@ -1,0 +1,149 @@
+"""The headline configuration at full size (BASELINE.json configs[2]): the
+10,000,002-triangle soup with the SBVH the bench builds, 1920x1080, max_depth 5.
+
+Bar: bit-exact against the oracle walking the same exported BVH2 with the reference algorithm
+(bvh-accelerator.h:488-547; pathtracer.h:61-164) — seeded closest-hit and any-hit traces (camera-like
+rays from the bench camera and rays from inside the soup), a strided tile subset of the frame
+rendered at 2 spp, and the deep-stack path: the counting kernel must see rays whose traversal stack
+went past the LDS-resident entries into the global overflow area.  At the full frame, where the
+oracle would take minutes, size-independent properties: every pixel holds exactly spp samples, and
+the frame is the same bit for bit whether rendered whole or as one rank's share of an 8-way split
+(pixels are independent, cpu/integrator.cpp:124).
+"""
+import numpy as np
+import pytest
+
+import py_oracle
+from akari_amd import capi, dist, scene
+from helpers import hits_to_gid, random_rays
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+W, H, TILE = 1920, 1080, 32
+
+
+@pytest.fixture(scope="module")
+def c3(hip_ctx_factory):
+    ctx = hip_ctx_factory(0)
+    cs = scene.compile_scene(scene.soup_scene(n_tris=10_000_000, resolution=(W, H)))
+    assert cs.n_tris == 10_000_002
+    info = scene.upload_scene(ctx, cs, builder=capi.BUILDER_SBVH, n_threads=16)
+    nodes, tris = ctx.accel_export()
+    assert len(tris) > cs.n_tris, "the SBVH duplicates references on the soup"
+    orc = py_oracle.OracleScene(cs, nodes, tris, capi)
+    yield ctx, cs, orc, info
+    ctx.close()
+
+
+def _camera_rays(cs, n, seed):
+    """Rays from the bench camera (0, 0, 4) through random points of the soup's bounding cube."""
+    rng = np.random.default_rng(seed)
+    r = np.zeros(n, capi.RAY_DTYPE)
+    o = np.asarray(cs.camera.position, np.float32)
+    target = rng.uniform(-1.01, 1.01, (n, 3)).astype(np.float32)
+    d = target - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    r["o"] = o
+    r["d"] = d
+    r["tmin"] = np.float32(1e-3)
+    r["tmax"] = np.float32(np.inf)
+    return r
+
+
+def _check(ctx, orc, cs, rays, any_hit, exact=False):
+    ctx.set_option("exact_cull", int(exact))
+    gh = ctx.trace(rays, any_hit=any_hit)
+    oh, _, _ = orc.trace(rays, any_hit=any_hit, exact_cull=exact, n_threads=16)
+    ctx.set_option("exact_cull", 0)
+    ggid = hits_to_gid(gh, cs.mesh_base)
+    bad = np.count_nonzero(ggid != oh["gid"])
+    assert bad == 0, f"{bad} of {len(rays)} hit ids differ"
+    hit = oh["gid"] != 0xFFFFFFFF
+    assert np.array_equal(gh["t"][hit], oh["t"][hit])
+    if not any_hit:
+        assert np.array_equal(gh["u"][hit], oh["u"][hit]) and np.array_equal(gh["v"][hit], oh["v"][hit])
+    return hit.mean()
+
+
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_c3_trace_bit_exact(c3, any_hit):
+    ctx, cs, orc, _ = c3
+    n = 1 << 17
+    frac_cam = _check(ctx, orc, cs, _camera_rays(cs, n, 100 + any_hit), any_hit)
+    frac_in = _check(ctx, orc, cs, random_rays(n, 200 + any_hit, -1.0, 1.0), any_hit)
+    assert frac_cam > 0.5 and frac_in > 0.5   # the rays really run through the soup
+
+
+def test_c3_trace_reference_cull_bit_exact(c3):
+    """The reference's own intersectAABB (AKR_PT_EXACT_CULL: no behind-origin cull, ~10x the box
+    tests) on a smaller batch."""
+    ctx, cs, orc, _ = c3
+    _check(ctx, orc, cs, random_rays(1 << 12, 300, -1.0, 1.0), False, exact=True)
+    _check(ctx, orc, cs, _camera_rays(cs, 1 << 12, 301), True, exact=True)
+
+
+def test_c3_deep_stack_overflow_path(c3):
+    """Rays whose traversal stack spills past the LDS entries (the global overflow area) are
+    present in the parity batches above and come out bit-exact."""
+    ctx, cs, orc, _ = c3
+    rays = np.concatenate([_camera_rays(cs, 1 << 16, 400), random_rays(1 << 16, 401, -1.0, 1.0)])
+    ctx.set_option("count_tests", 1)
+    ctx.reset_stats()
+    try:
+        _check(ctx, orc, cs, rays, False)
+        deep = ctx.trace_counts()["per_mode"]["closest"]["deep_rays"]
+        ctx.reset_stats()
+        _check(ctx, orc, cs, rays, True)
+        deep_any = ctx.trace_counts()["per_mode"]["any"]["deep_rays"]
+    finally:
+        ctx.set_option("count_tests", 0)
+        ctx.reset_stats()
+    assert deep > 0, "no closest-hit ray reached the overflow stack"
+    print(f"deep-stack rays: closest {deep}, any-hit {deep_any} of {len(rays)}")
+
+
+def test_c3_render_tile_subset_bit_exact(c3):
+    """Every 64th 32x32 tile of the 1080p frame, 2 spp, max_depth 5, through the C-ABI."""
+    ctx, cs, orc, _ = c3
+    tiles = dist.tiles_for_rank(W, H, TILE, 0, 64)
+    rad, w = ctx.render(2, 5, tiles, W, H)
+    orad, ow, st = orc.render(2, 5, tiles=tiles, n_threads=16)
+    assert np.array_equal(w, ow)
+    assert (ow > 0).sum() == dist.n_pixels(tiles)
+    diff = np.abs(rad - orad).max()
+    assert np.array_equal(rad, orad), f"radiance differs (max abs diff {diff})"
+    # NEE runs (shadow rays are traced), though the 1-cm mean free path of the soup occludes the
+    # emitter above it from everything the camera sees: the C3 frame is dark by construction
+    assert st["shadow_rays"] > 0 and st["extension_rays"] > 0
+
+
+def test_c3_full_frame_split_invariance(c3):
+    """Full 1080p frame at 1 spp on the device: every pixel holds one sample (the library's in-band
+    check runs too), and rank 3's share of an 8-way tile split renders the same bits as the same
+    pixels of the whole frame."""
+    import torch
+    ctx, cs, orc, _ = c3
+    dev = torch.device("cuda", 0)
+    full = dist.tile_grid(W, H, TILE)
+    n = dist.n_pixels(full)
+    film = torch.zeros(4 * n, device=dev)
+    ctx.render_device(1, 5, full, film[:3 * n].data_ptr(), film[3 * n:].data_ptr(),
+                      torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    packed = film.cpu().numpy()
+    assert np.all(packed[3 * n:] == 1.0)
+    frame = np.zeros((H, W, 3), np.float32)
+    fw = np.zeros((H, W), np.float32)
+    dist.unpack_to_frame(packed, full, W, H, frame, fw)
+    share = dist.tiles_for_rank(W, H, TILE, 3, 8)
+    m = dist.n_pixels(share)
+    sfilm = torch.zeros(4 * m, device=dev)
+    ctx.render_device(1, 5, share, sfilm[:3 * m].data_ptr(), sfilm[3 * m:].data_ptr(),
+                      torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    sframe = np.zeros((H, W, 3), np.float32)
+    sw = np.zeros((H, W), np.float32)
+    dist.unpack_to_frame(sfilm.cpu().numpy(), share, W, H, sframe, sw)
+    sel = sw > 0
+    assert sel.sum() == m
+    assert np.array_equal(sframe[sel], frame[sel])

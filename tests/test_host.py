@@ -150,6 +150,11 @@ def test_wide_view_preorder_parallel(builder):
     assert len(wn) > 3 * 4096
     _, _, _, (wn2, lv2, root2) = capi.build_bvh_host(cs.vertices, cs.indices, wide=True, builder=b)
     assert root == root2 == 0 and wn.tobytes() == wn2.tobytes() and lv.tobytes() == lv2.tobytes()
+    # the serial build (one thread: BVH2 build and the whole collapse on the calling thread) agrees
+    # byte for byte with the default thread pool
+    n1, t1, _, (wn1, lv1, root1) = capi.build_bvh_host(cs.vertices, cs.indices, wide=True, builder=b, n_threads=1)
+    assert n1.tobytes() == nodes.tobytes() and t1.tobytes() == tris.tobytes()
+    assert root1 == 0 and wn1.tobytes() == wn.tobytes() and lv1.tobytes() == lv.tobytes()
     next_node, next_leaf = [0], [0]
     stack = [root]
     while stack:
@@ -230,6 +235,27 @@ def test_oracle_render_tiles_accumulate_and_threads():
     assert np.array_equal(full, r) and np.array_equal(wf, w)
     r2, w2, _ = orc.render(3, 5, tiles=part, radiance=r.copy(), weight=w.copy())
     assert np.array_equal(r2, 2 * full) and np.all(w2 == 6)
+
+
+def test_oracle_overlapping_tiles_merge_in_tile_order():
+    """Overlapping tiles are merged one after another in tile order (Film::merge_tile under the
+    reference's mutex, cpu/integrator.cpp:138-140; the HIP library merges in the same order): the
+    same tile listed 8 times on 8 threads is the single render added 8 times, every pixel, every
+    run.  An unlocked merge from the worker threads lost updates here (the r1 flaky weights)."""
+    cs = scene.compile_scene(cornell((32, 32)))
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    orc = O.OracleScene(cs, nodes, tris, capi)
+    t = (3, 2, 29, 31)
+    one, w1, _ = orc.render(2, 5, tiles=[t], n_threads=1)
+    acc = np.zeros_like(one)
+    for _ in range(8):
+        acc = (acc + one).astype(np.float32)
+    for _ in range(3):
+        r, w, _ = orc.render(2, 5, tiles=[t] * 8, n_threads=8)
+        assert np.array_equal(w, 8 * w1) and np.array_equal(r, acc)
+    ao1, aw1, _ = orc.render_ao(3, tiles=[t], n_threads=1)
+    ao, aw, _ = orc.render_ao(3, tiles=[t] * 8, n_threads=8)
+    assert np.array_equal(aw, 8 * aw1) and np.array_equal(ao, 8 * ao1)
 
 
 def test_oracle_ao_properties():
