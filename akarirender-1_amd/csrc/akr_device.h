@@ -127,6 +127,7 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
                                    // (3 x float4 each); wide leaf refs hold the float4 offset
     uint32_t wide_root;            // wide reference of the real root
     uint32_t lean;                 // 1: lean slot tests allowed (wide view's frames bounded by 2^40)
+    uint32_t any_far_first;        // 1: shadow (boolean occlusion) rays visit the far slots first (order-free)
     TraceCounters *counters;       // [3]: closest, any, shadow
     uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
 };
@@ -231,6 +232,33 @@ struct SplatArgs {
     float ray_clamp;
     uint32_t lookahead;            // nonzero: per active pixel of `look`, its accepted lanes in chain order
     LookArgs look;
+};
+
+// k_path counting build: per-wave phase profile (wall clock, 100 MHz), summed over waves
+struct PathProfile {
+    unsigned long long waves;      // waves that ran
+    unsigned long long outer;      // outer iterations
+    unsigned long long procs;      // processing phases (A)
+    unsigned long long trav_iters; // traversal-loop iterations (B)
+    unsigned long long t_proc, t_trav, t_leaf, t_total;  // ticks in A, B, C, and the whole wave
+    unsigned long long t_max;      // longest wave (atomicMax)
+    unsigned long long lanes_proc; // waiting lanes processed, summed over phases
+    unsigned long long t_shade;    // ticks of A spent on finished rays' results (shading, shadow hand-over)
+};
+
+// Persistent path kernel (k_path): the whole sample loop of every pixel of the tile list.
+struct PathArgs {
+    TraceArgs t;                   // BVH, wide view, overflow stacks, counters
+    SceneDev sc;
+    CameraDev cam;
+    const uint32_t *pixel;         // per slot: x | y << 16
+    float4 *film;                  // per slot: (rgb sums, weight), written when the pixel's samples are done
+    uint32_t *work;                // kWorkShards pixel-fetch counters, kWorkStride apart (zeroed before)
+    uint32_t n_pix, spp;
+    int32_t max_depth;
+    float ray_clamp;
+    uint32_t min_wait;             // a wave processes its waiting lanes once this many wait (or half its live lanes)
+    PathProfile *prof;             // counting build only
 };
 
 }  // namespace akr

@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "akr_trig.h"
 
 namespace akr {
 
@@ -49,9 +50,14 @@ __device__ __forceinline__ V2 lerp3(V2 a, V2 b, V2 c, float u, float v) {
     float w = 1.0f - u - v;
     return {(a.x * w + b.x * u) + c.x * v, (a.y * w + b.y * u) + c.y * v};
 }
-// Scalar sin/cos in f64 rounded to f32 (the correctly rounded f32 value), see DESIGN.md §4.
-__device__ __forceinline__ float fsin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float fcos(float x) { return (float)cos((double)x); }
+// Scalar sin/cos in f64 rounded to f32 (the correctly rounded f32 value), see DESIGN.md §4;
+// akr_trig.h's bounded-range f64 kernels (identical to glibc's f64 results after rounding on every
+// f32 in [-2 pi, 2 pi], tests/test_host.py).
+#ifdef AKR_PROBE_F32TRIG  // timing probe only (not bit-exact): the f32 library functions
+__device__ __forceinline__ void fsincos(float x, float &s, float &c) { s = sinf(x); c = cosf(x); }
+#else
+__device__ __forceinline__ void fsincos(float x, float &s, float &c) { trig_sincosf(x, s, c); }
+#endif
 
 // LCGSampler::next1d (kernel/sampler.h:60-63)
 __device__ __forceinline__ float lcg_next(uint32_t &s) {
@@ -97,7 +103,9 @@ __device__ __forceinline__ V2 concentric_disk(V2 u) {
         r = o.y;
         theta = kPi2 - kPi4 * (o.x / o.y);
     }
-    return {r * fcos(theta), r * fsin(theta)};
+    float s, c;
+    fsincos(theta, s, c);
+    return {r * c, r * s};
 }
 __device__ __forceinline__ V3 cosine_hemisphere(V2 u) {
     V2 d = concentric_disk(u);
@@ -164,7 +172,9 @@ __device__ __forceinline__ V3 closure_sample(const Closure &c, V2 u, V3 wo, V3 &
     float t2 = c.alpha * c.alpha * u.x / (1 - u.x);
     float cos_t = 1.0f / sqrtf(1 + t2);
     float sin_t = sqrtf(rmax(0.0f, 1 - cos_t * cos_t));
-    V3 wh = v3(fcos(phi) * sin_t, cos_t, fsin(phi) * sin_t);
+    float sp, cp;
+    fsincos(phi, sp, cp);
+    V3 wh = v3(cp * sin_t, cos_t, sp * sin_t);
     if (!same_hemisphere(wo, wh)) wh = neg(wh);
     wi = add(muls(wo, -1.0f), muls(wh, 2.0f * dot(wo, wh)));
     if (!same_hemisphere(wo, wi)) {

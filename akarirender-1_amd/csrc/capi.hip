@@ -233,6 +233,10 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
+    uint32_t path_grid = 0;   // resident workgroups of the persistent path kernel
+    bool path_kernel = true;  // option "path": render with k_path (false: the wavefront kernels)
+    bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
+    int path_min_wait = 32;   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
     DBuf<float4> d_trace_rays;
     DBuf<akr_hit> d_trace_hits;
 
@@ -248,6 +252,7 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_steps;
     uint64_t n_steps = 0;
     DBuf<TraceCounters> d_counters;
+    DBuf<PathProfile> d_pprof;  // k_path counting build: per-wave phase profile
     std::vector<hipEvent_t> pool;
     struct Pending {
         const char *name;
@@ -290,7 +295,7 @@ struct akr_hip_ctx {
 
     template <class F>
     void timed(const char *name, hipStream_t st, F &&launch) {
-        if (!stats || (stats_closest_only && std::strcmp(name, "trace_closest") != 0)) {
+        if (!stats || (stats_closest_only && std::strcmp(name, "trace_closest") != 0 && std::strcmp(name, "path") != 0)) {
             launch();
             return;
         }
@@ -438,6 +443,8 @@ struct akr_hip_ctx {
             trace_grid[m] = (uint32_t)(n_cu * trace_blocks_per_cu(m));
             mx = std::max(mx, trace_grid[m]);
         }
+        path_grid = (uint32_t)(n_cu * path_blocks_per_cu());
+        mx = std::max(mx, path_grid);
         ovf_threads = mx * kTraceBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_ovf_side.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
@@ -503,6 +510,7 @@ struct akr_hip_ctx {
         t.wide_root = wide_root_dev;
         // the lean slot test's slack is derived for frame origins and steps below 2^40
         t.lean = lean && bvh4.max_abs <= 0x1p40f ? 1u : 0u;
+        t.any_far_first = any_far_first ? 1u : 0u;
         t.tris = d_tris.p;
         t.stack_ovf = d_ovf.p;
         t.ovf_threads = ovf_threads;
@@ -521,6 +529,8 @@ struct akr_hip_ctx {
             if (!d_counters.p) {
                 d_counters.reserve(3);
                 HIPCHK(hipMemset(d_counters.p, 0, 3 * sizeof(TraceCounters)));
+                d_pprof.reserve(1);
+                HIPCHK(hipMemset(d_pprof.p, 0, sizeof(PathProfile)));
             }
         }
     }
@@ -715,6 +725,33 @@ struct akr_hip_ctx {
         }
         const SceneDev sd = scene_dev();
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
+        // Persistent path kernel: every sample of every pixel in one launch.  It
+        // runs the lean wide traversal only; the reference cull, the BVH2 kernel, a wide view whose
+        // frames exceed the lean test's bounds and lookahead lanes keep the wavefront form.
+        if (path_kernel && tight && wide && !la && trace_args(nullptr).lean) {
+            if (p.spp > 0) {
+                HIPCHK(hipMemsetAsync(d_counts.p, 0, kWorkWords * sizeof(uint32_t), ms));
+                PathArgs pa{};
+                pa.t = trace_args(nullptr);
+                pa.sc = sd;
+                pa.cam = cam;
+                pa.pixel = d_pixel.p;
+                pa.film = d_film.p;
+                pa.work = d_counts.p;
+                pa.n_pix = (uint32_t)N;
+                pa.spp = (uint32_t)p.spp;
+                pa.max_depth = p.max_depth;
+                pa.ray_clamp = p.ray_clamp;
+                pa.min_wait = (uint32_t)path_min_wait;
+                pa.prof = count ? d_pprof.p : nullptr;
+                const uint32_t grid = (uint32_t)std::min<uint64_t>(path_grid, (N + kTraceBlock - 1) / kTraceBlock);
+                timed("path", ms, [&] { launch_path(count, pa, grid, ms); });
+                HIPCHK(hipGetLastError());
+            }
+            last_passes = 1;
+            join_streams(st);
+            return N;
+        }
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
         int64_t g = 0;  // bounce index over all passes: shadow queues alternate by its parity
@@ -951,7 +988,7 @@ const char *akr_hip_last_error(const akr_hip_ctx *ctx) { return ctx ? ctx->err.c
 int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
     return guard(ctx, [&] {
         std::string k = key ? key : "";
-        if (k == "stats") {  // 1: every kernel; 2: the dominant kernel (trace_closest) only
+        if (k == "stats") {  // 1: every kernel; 2: the dominant kernel (trace_closest, or path) only
             ctx->stats = value != 0;
             ctx->stats_closest_only = value == 2;
         } else if (k == "exact_cull") {
@@ -971,6 +1008,13 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             if (value < 0 || value > (int64_t)kLookMaxLanes)
                 throw std::runtime_error("lookahead must be in [0, 64] (0 = auto, 1 = off, n = on with at most n lanes)");
             ctx->lookahead = (int)value;
+        } else if (k == "path") {
+            ctx->path_kernel = value != 0;
+        } else if (k == "any_far_first") {
+            ctx->any_far_first = value != 0;
+        } else if (k == "path_min_wait") {
+            if (value < 1 || value > 64) throw std::runtime_error("path_min_wait must be in [1, 64]");
+            ctx->path_min_wait = (int)value;
         } else if (k == "verify") {
             ctx->verify = value != 0;
         } else if (k == "la_early_exit") {
@@ -1412,6 +1456,17 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
     });
 }
 
+int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n) {
+    return guard(ctx, [&] {
+        if (!out || n < 0) throw std::runtime_error("null output");
+        PathProfile q{};
+        if (ctx->d_pprof.p) HIPCHK(hipMemcpy(&q, ctx->d_pprof.p, sizeof(q), hipMemcpyDeviceToHost));
+        const uint64_t v[] = {q.waves, q.outer, q.procs, q.trav_iters, q.t_proc, q.t_trav, q.t_leaf, q.t_total, q.t_max,
+                              q.lanes_proc, q.t_shade};
+        for (int32_t k = 0; k < n && k < (int32_t)(sizeof(v) / sizeof(v[0])); k++) out[k] = v[k];
+    });
+}
+
 int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes) {
     return guard(ctx, [&] {
         if (lanes) *lanes = ctx->last_lanes;
@@ -1425,6 +1480,7 @@ int akr_hip_reset_stats(akr_hip_ctx *ctx) {
         ctx->flush_stats();
         ctx->stat.clear();
         if (ctx->d_counters.p) HIPCHK(hipMemset(ctx->d_counters.p, 0, 3 * sizeof(TraceCounters)));
+        if (ctx->d_pprof.p) HIPCHK(hipMemset(ctx->d_pprof.p, 0, sizeof(PathProfile)));
     });
 }
 

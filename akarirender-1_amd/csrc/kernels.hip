@@ -425,17 +425,18 @@ __device__ __forceinline__ void emit_result(const TraceArgs &a, uint32_t idx, fl
 // the rare rays the wide kernel cannot take (fast_box_ok false: a zero or denormal direction
 // component, a non-finite origin or a NaN interval).  Runs inline while the rest of the wave
 // waits, so no extra launch is ever needed; the lane's LDS stack is free (it holds no ray).
-template <int MODE, bool TIGHT>
-__device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t idx, V3 o, V3 d, V3 invd, float tmin,
-                                              float tmax, lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid) {
-    constexpr bool ANY = MODE != TRACE_CLOSEST;
+template <bool ANY, bool TIGHT>
+__device__ __forceinline__ void trace_exact_core(const TraceArgs &a, V3 o, V3 d, V3 invd, float tmin, float tmax,
+                                                 lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid, float &best,
+                                                 float &bu, float &bv, uint32_t &bgid, bool &occluded) {
     const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
     const uint4 *nodesu = reinterpret_cast<const uint4 *>(a.nodes);
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const uint32_t root = nodesu[3].x;
-    float best = kInf, bu = 0.0f, bv = 0.0f;
-    uint32_t bgid = kNoHit;
-    bool occluded = false;
+    best = kInf;
+    bu = bv = 0.0f;
+    bgid = kNoHit;
+    occluded = false;
     int sp = 0;
     const float tr = box_test<TIGHT, false>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
     uint32_t cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
@@ -465,6 +466,16 @@ __device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t id
         if (ANY && occluded) break;
         cur = stack_pop(s_stack, ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
     }
+}
+
+template <int MODE, bool TIGHT>
+__device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t idx, V3 o, V3 d, V3 invd, float tmin,
+                                              float tmax, lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid) {
+    float best, bu, bv;
+    uint32_t bgid;
+    bool occluded;
+    trace_exact_core<MODE != TRACE_CLOSEST, TIGHT>(a, o, d, invd, tmin, tmax, s_stack, ovf, tid, gtid, best, bu, bv, bgid,
+                                                   occluded);
     emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
 }
 
@@ -674,6 +685,9 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             tmax = rb.w;
             invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
             dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
+            // boolean occlusion (shadow mode): far slots first — the answer is order-free;
+            // the ABI's any-hit query reports the t of the hit it finds, so it keeps the BVH2 order
+            if (MODE == TRACE_SHADOW && a.any_far_first) dpos ^= 7u;
             if (WIDE && TIGHT) {
                 lean = a.lean && lean_ok(o, invd, tmin, tmax);
                 tmaxp = float_below(tmax);
@@ -1028,8 +1042,142 @@ __device__ __forceinline__ V3 tex_eval(const SceneDev &s, int32_t ti, V2 tc) {
 
 __device__ __forceinline__ V3 ld3(const float *p) { return v3(p[0], p[1], p[2]); }
 
-// One bounce of GenericPathTracer::run_megakernel for every queued hit (pathtracer.h:137-162):
-// on_surface_scatter (:96-132) then compute_direct_lighting(select_light) (:65-91).
+// One bounce of GenericPathTracer::run_megakernel at a closest hit (pathtracer.h:137-162):
+// on_surface_scatter (:96-132) then compute_direct_lighting(select_light) (:65-91).  Shared by the
+// wavefront shade kernel and the persistent path kernel, so both run the same arithmetic.
+struct Bounce {
+    bool emit;        // L += e (depth 0, front-facing or double-sided emitter)
+    V3 e;
+    bool ext;         // next ray (e0 = p | tmin, e1 = wi | tmax) with throughput nb
+    float4 e0, e1;
+    V3 nb;
+    bool sh;          // shadow ray (s0 = light point | tmin, s1 = direction | tmax), contribution col
+    float4 s0, s1;
+    V3 col;
+};
+
+__device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
+                                          uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
+    o.emit = o.ext = o.sh = false;
+    const ShadeTri tr = s.tri[gid];
+    const int32_t mid = (int32_t)fbits(tr.a.w);
+    if (mid < 0) return;  // a null material ends the path (undefined in the reference)
+    const V3 v0{tr.a.x, tr.a.y, tr.a.z}, v1{tr.b.x, tr.b.y, tr.b.z}, v2{tr.c.x, tr.c.y, tr.c.z};
+    // SurfaceInteraction(uv, triangle) (interaction.h:40-41, shape.h:31-40)
+    const V3 p = lerp3(v0, v1, v2, u, v);
+    const V3 ng = normalize(cross(sub(v1, v0), sub(v2, v0)));
+    const V3 ns = lerp3(v3(tr.b.w, tr.c.w, tr.d.x), v3(tr.d.y, tr.d.z, tr.d.w), v3(tr.e.x, tr.e.y, tr.e.z), u, v);
+    V2 tc{0.0f, 0.0f};  // only textures read it; constant textures ignore it
+    if (s.has_image_tex) {
+        const float *tt = s.texcoords + 6 * (size_t)gid;
+        tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
+    }
+    const akr_material *mat = &s.mats[mid];
+    if (mat->type == AKR_MAT_EMISSIVE) {
+        if (depth == 0) {
+            const bool face_front = dot(neg(wo), ng) < 0.0f;
+            if (mat->double_sided || face_front) {
+                o.emit = true;
+                o.e = mul(beta, tex_eval(s, mat->color, tc));
+            }
+        }
+        return;
+    }
+    if (depth >= max_depth) return;
+    // MaterialEvalContext holds a COPY of the sampler: u1.x is the next draw
+    uint32_t copy = seed;
+    float sel_u = lcg_next(copy);
+    float choice_pdf = 1.0f;
+    while (mat->type == AKR_MAT_MIX) {  // Material::select_material, material.h:251-268
+        const float frac = tex_eval(s, mat->fraction, tc).x;
+        if (sel_u < frac) {
+            sel_u = sel_u / frac;
+            mat = &s.mats[mat->second];
+            choice_pdf *= 1.0f / frac;
+        } else {
+            sel_u = (sel_u - frac) / (1.0f - frac);
+            mat = &s.mats[mat->first];
+            choice_pdf *= 1.0f / (1.0f - frac);
+        }
+    }
+    Closure cl{CL_NONE, v3(0, 0, 0), 0.0f};
+    if (mat->type == AKR_MAT_DIFFUSE) {
+        cl.kind = CL_DIFFUSE;
+        cl.R = tex_eval(s, mat->color, tc);
+    } else if (mat->type == AKR_MAT_GLOSSY) {
+        cl.kind = CL_GLOSSY;
+        cl.R = tex_eval(s, mat->color, tc);
+        float r = tex_eval(s, mat->roughness, tc).x;
+        r *= r;
+        cl.alpha = r;
+    }
+    const Frame frame = make_frame(ns);
+    const V2 bu = lcg_next2(seed);  // BSDFSampleContext(sampler.next2d(), wo)
+    if (cl.kind == CL_NONE) return;
+    V3 wi_l;
+    float pdf = 0.0f;
+    const V3 f = closure_sample(cl, bu, to_local(frame, wo), wi_l, pdf);
+    const V3 wi = to_world(frame, wi_l);
+    pdf *= choice_pdf;
+    if (pdf == 0.0f) return;
+    const float cng = fabsf(dot(ng, wi));
+    const V3 ev_beta = divs(muls(f, cng), pdf);
+    // select_light(sampler.next2d()) — scene.h:79-90
+    const V2 su = lcg_next2(seed);
+    if (s.n_lights > 0) {
+        int lo = 0, hi = s.n_lights + 1;  // upper_bound, distribution.h:32-44
+        while (lo < hi) {
+            const int m = (lo + hi) / 2;
+            if (s.light_cdf[m] <= su.x) lo = m + 1; else hi = m;
+        }
+        int li = hi - 1;
+        li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
+        const float sel_pdf = s.light_func[li] / (s.light_func_int * (float)s.n_lights);
+        const LightDev &lt = s.lights[li];
+        const V2 lu = lcg_next2(seed);
+        // AreaLight::sample (light.h:58-71)
+        const float su0 = sqrtf(lu.x);
+        const float b0 = 1 - su0, b1 = lu.y * su0;
+        const V3 l0 = ld3(lt.v), l1 = ld3(lt.v + 3), l2 = ld3(lt.v + 6);
+        const V3 lp = lerp3(l0, l1, l2, b0, b1);
+        const V3 lx = cross(sub(l1, l0), sub(l2, l0));
+        const V3 lng = normalize(lx);
+        V3 lwi = sub(lp, p);
+        const float dist_sqr = dot(lwi, lwi);
+        lwi = divs(lwi, sqrtf(dist_sqr));
+        const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]}, V2{lt.tc[4], lt.tc[5]}, b0, b1);
+        const V3 Le = tex_eval(s, lt.color_tex, ltc);
+        const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / (length(lx) * 0.5f);
+        if (!(lpdf <= 0.0f)) {
+            const float light_pdf = sel_pdf * lpdf;
+            const V3 fe = closure_eval(cl, to_local(frame, wo), to_local(frame, lwi));
+            const V3 fl = muls(mul(Le, fe), fabsf(dot(ns, lwi)));
+            const V3 col = divs(mul(beta, fl), light_pdf);
+            if (!is_black(col)) {
+                o.sh = true;
+                const V3 sd = neg(lwi);
+                o.s0 = make_float4(lp.x, lp.y, lp.z, kEps / fabsf(dot(lwi, lng)));
+                o.s1 = make_float4(sd.x, sd.y, sd.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
+                o.col = col;
+            }
+        }
+    }
+    if (!last) {
+        o.ext = true;
+        o.nb = mul(beta, ev_beta);
+        o.e0 = make_float4(p.x, p.y, p.z, kEps / cng);
+        o.e1 = make_float4(wi.x, wi.y, wi.z, kInf);
+    }
+}
+
+// Out-of-line copy for the persistent path kernel: a call keeps the shading code's registers out of
+// the traversal loop's allocation (the caller saves its few live values around the call).
+__device__ __noinline__ void shade_hit_call(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
+                                            uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
+    shade_hit(s, gid, u, v, wo, beta, seed, depth, max_depth, last, o);
+}
+
+// One bounce for every queued hit (wavefront form)
 #ifndef AKR_SHADE_BLOCK
 #define AKR_SHADE_BLOCK 256
 #endif
@@ -1038,156 +1186,43 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(ShadeArgs a) {
     const uint32_t i = blockIdx.x * kShadeBlock + threadIdx.x;
     const uint32_t n = *a.count_in;
     if (blockIdx.x * kShadeBlock >= n) return;  // whole workgroup past the queue (uniform: before any barrier)
-    bool want_ext = false, want_sh = false;
-    float4 e0 = {}, e1 = {}, st_out = {}, s0 = {}, s1 = {}, sc = {};
-    uint32_t slot = 0;
+    Bounce bo;
+    bo.ext = bo.sh = false;
+    uint32_t slot = 0, seed = 0;
     if (i < n) {
         slot = a.slot_in[i];
         const float4 stv = a.state_in[i];
-        uint32_t seed = fbits(stv.w);
-        const V3 beta{stv.x, stv.y, stv.z};
+        seed = fbits(stv.w);
         const float4 hv = a.hit_in[i];
         const uint32_t gid = fbits(hv.w);
         if (gid != kNoHit) {  // miss -> on_miss (no-op), the path ends
-            const SceneDev &s = a.sc;
-            const ShadeTri tr = s.tri[gid];
-            const int32_t mid = (int32_t)fbits(tr.a.w);
-            if (mid >= 0) {  // a null material ends the path (undefined in the reference)
-                const float4 rdv = a.ray_in[2 * (size_t)i + 1];
-                const V3 wo = neg(v3(rdv.x, rdv.y, rdv.z));
-                const float u = hv.y, v = hv.z;
-                const V3 v0{tr.a.x, tr.a.y, tr.a.z}, v1{tr.b.x, tr.b.y, tr.b.z}, v2{tr.c.x, tr.c.y, tr.c.z};
-                // SurfaceInteraction(uv, triangle) (interaction.h:40-41, shape.h:31-40)
-                const V3 p = lerp3(v0, v1, v2, u, v);
-                const V3 ng = normalize(cross(sub(v1, v0), sub(v2, v0)));
-                const V3 ns = lerp3(v3(tr.b.w, tr.c.w, tr.d.x), v3(tr.d.y, tr.d.z, tr.d.w), v3(tr.e.x, tr.e.y, tr.e.z),
-                                    u, v);
-                V2 tc{0.0f, 0.0f};  // only textures read it; constant textures ignore it
-                if (s.has_image_tex) {
-                    const float *tt = s.texcoords + 6 * (size_t)gid;
-                    tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
-                }
-                const akr_material *mat = &s.mats[mid];
-                if (mat->type == AKR_MAT_EMISSIVE) {
-                    if (a.depth == 0) {
-                        const bool face_front = dot(neg(wo), ng) < 0.0f;
-                        if (mat->double_sided || face_front) {
-                            const V3 e = mul(beta, tex_eval(s, mat->color, tc));
-                            float4 l = a.L[slot];
-                            l.x += e.x;
-                            l.y += e.y;
-                            l.z += e.z;
-                            a.L[slot] = l;
-                        }
-                    }
-                } else if (a.depth < a.max_depth) {
-                    // MaterialEvalContext holds a COPY of the sampler: u1.x is the next draw
-                    uint32_t copy = seed;
-                    float sel_u = lcg_next(copy);
-                    float choice_pdf = 1.0f;
-                    while (mat->type == AKR_MAT_MIX) {  // Material::select_material, material.h:251-268
-                        const float frac = tex_eval(s, mat->fraction, tc).x;
-                        if (sel_u < frac) {
-                            sel_u = sel_u / frac;
-                            mat = &s.mats[mat->second];
-                            choice_pdf *= 1.0f / frac;
-                        } else {
-                            sel_u = (sel_u - frac) / (1.0f - frac);
-                            mat = &s.mats[mat->first];
-                            choice_pdf *= 1.0f / (1.0f - frac);
-                        }
-                    }
-                    Closure cl{CL_NONE, v3(0, 0, 0), 0.0f};
-                    if (mat->type == AKR_MAT_DIFFUSE) {
-                        cl.kind = CL_DIFFUSE;
-                        cl.R = tex_eval(s, mat->color, tc);
-                    } else if (mat->type == AKR_MAT_GLOSSY) {
-                        cl.kind = CL_GLOSSY;
-                        cl.R = tex_eval(s, mat->color, tc);
-                        float r = tex_eval(s, mat->roughness, tc).x;
-                        r *= r;
-                        cl.alpha = r;
-                    }
-                    const Frame frame = make_frame(ns);
-                    const V2 bu = lcg_next2(seed);  // BSDFSampleContext(sampler.next2d(), wo)
-                    if (cl.kind != CL_NONE) {
-                        V3 wi_l;
-                        float pdf = 0.0f;
-                        const V3 f = closure_sample(cl, bu, to_local(frame, wo), wi_l, pdf);
-                        const V3 wi = to_world(frame, wi_l);
-                        pdf *= choice_pdf;
-                        if (pdf != 0.0f) {
-                            const float cng = fabsf(dot(ng, wi));
-                            const V3 ev_beta = divs(muls(f, cng), pdf);
-                            // select_light(sampler.next2d()) — scene.h:79-90
-                            const V2 su = lcg_next2(seed);
-                            if (s.n_lights > 0) {
-                                int lo = 0, hi = s.n_lights + 1;  // upper_bound, distribution.h:32-44
-                                while (lo < hi) {
-                                    const int m = (lo + hi) / 2;
-                                    if (s.light_cdf[m] <= su.x) lo = m + 1; else hi = m;
-                                }
-                                int li = hi - 1;
-                                li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
-                                const float sel_pdf = s.light_func[li] / (s.light_func_int * (float)s.n_lights);
-                                const LightDev &lt = s.lights[li];
-                                const V2 lu = lcg_next2(seed);
-                                // AreaLight::sample (light.h:58-71)
-                                const float su0 = sqrtf(lu.x);
-                                const float b0 = 1 - su0, b1 = lu.y * su0;
-                                const V3 l0 = ld3(lt.v), l1 = ld3(lt.v + 3), l2 = ld3(lt.v + 6);
-                                const V3 lp = lerp3(l0, l1, l2, b0, b1);
-                                const V3 lx = cross(sub(l1, l0), sub(l2, l0));
-                                const V3 lng = normalize(lx);
-                                V3 lwi = sub(lp, p);
-                                const float dist_sqr = dot(lwi, lwi);
-                                lwi = divs(lwi, sqrtf(dist_sqr));
-                                const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]},
-                                                     V2{lt.tc[4], lt.tc[5]}, b0, b1);
-                                const V3 Le = tex_eval(s, lt.color_tex, ltc);
-                                const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / (length(lx) * 0.5f);
-                                if (!(lpdf <= 0.0f)) {
-                                    const float light_pdf = sel_pdf * lpdf;
-                                    const V3 fe = closure_eval(cl, to_local(frame, wo), to_local(frame, lwi));
-                                    const V3 fl = muls(mul(Le, fe), fabsf(dot(ns, lwi)));
-                                    const V3 col = divs(mul(beta, fl), light_pdf);
-                                    if (!is_black(col)) {
-                                        want_sh = true;
-                                        const V3 sd = neg(lwi);
-                                        s0 = make_float4(lp.x, lp.y, lp.z, kEps / fabsf(dot(lwi, lng)));
-                                        s1 = make_float4(sd.x, sd.y, sd.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
-                                        sc = make_float4(col.x, col.y, col.z, bitsf(slot));
-                                    }
-                                }
-                            }
-                            const V3 nb = mul(beta, ev_beta);
-                            if (!a.last) {
-                                want_ext = true;
-                                e0 = make_float4(p.x, p.y, p.z, kEps / cng);
-                                e1 = make_float4(wi.x, wi.y, wi.z, kInf);
-                                st_out = make_float4(nb.x, nb.y, nb.z, bitsf(seed));
-                            }
-                        }
-                    }
-                }
+            const float4 rdv = a.ray_in[2 * (size_t)i + 1];
+            shade_hit(a.sc, gid, hv.y, hv.z, neg(v3(rdv.x, rdv.y, rdv.z)), V3{stv.x, stv.y, stv.z}, seed, a.depth,
+                      a.max_depth, a.last != 0, bo);
+            if (bo.emit) {
+                float4 l = a.L[slot];
+                l.x += bo.e.x;
+                l.y += bo.e.y;
+                l.z += bo.e.z;
+                a.L[slot] = l;
             }
         }
         // the path does not reach another traced bounce: persist its sampler stream for the next
         // sample pass (the stream continues across spp, cpu/integrator.cpp:124-134)
-        if (!want_ext) a.seed[slot] = seed;
+        if (!bo.ext) a.seed[slot] = seed;
     }
     uint32_t pos, spos;
-    block_append2<kShadeBlock>(want_ext, a.count_out, pos, want_sh, a.shadow_count, spos);
-    if (want_ext) {
-        a.ray_out[2 * (size_t)pos] = e0;
-        a.ray_out[2 * (size_t)pos + 1] = e1;
-        a.state_out[pos] = st_out;
+    block_append2<kShadeBlock>(bo.ext, a.count_out, pos, bo.sh, a.shadow_count, spos);
+    if (bo.ext) {  // the seed travels with the path state
+        a.ray_out[2 * (size_t)pos] = bo.e0;
+        a.ray_out[2 * (size_t)pos + 1] = bo.e1;
+        a.state_out[pos] = make_float4(bo.nb.x, bo.nb.y, bo.nb.z, bitsf(seed));
         a.slot_out[pos] = slot;
     }
-    if (want_sh) {
-        a.shadow_ray[2 * (size_t)spos] = s0;
-        a.shadow_ray[2 * (size_t)spos + 1] = s1;
-        a.shadow_color[spos] = sc;
+    if (bo.sh) {
+        a.shadow_ray[2 * (size_t)spos] = bo.s0;
+        a.shadow_ray[2 * (size_t)spos + 1] = bo.s1;
+        a.shadow_color[spos] = make_float4(bo.col.x, bo.col.y, bo.col.z, bitsf(slot));
     }
 }
 
@@ -1280,6 +1315,391 @@ __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
     float4 f = a.film[i];
     splat_one(f, a.L[i], a.ray_clamp);
     a.film[i] = f;
+}
+
+// ------------------------------------------------------------------------------ persistent path
+// k_path: the whole per-pixel sample loop of cpu::PathTracer::render (cpu/integrator.cpp:89-142,
+// run_megakernel pathtracer.h:133-164) in one persistent launch.  A lane owns one pixel at a time
+// and runs its spp samples in order, so the sampler stream, the order of the L additions and the
+// film sums are exactly the sequential loop's; it takes the next pixel from the XCD-sharded pixel
+// counters when it finishes one.  Per outer iteration a wave
+//   A. processes the lanes whose ray has finished, once enough of them wait: a shadow ray adds its
+//      contribution and hands over to the pending extension ray; a closest hit is shaded inline
+//      (shade_hit), which yields a shadow ray (traced first) and/or the next extension ray; a
+//      finished sample is splatted into the pixel's film sums and the next camera ray is made;
+//   B. runs the traversal phase of k_trace's while-while loop (lean wide slot tests, speculative
+//      leaves, early exit) over every lane's current ray, closest-hit or shadow alike;
+//   C. runs the leaf phase.
+// No launch boundary separates the bounces of a pixel from those of its neighbours, so a slow ray
+// delays only its own pixel's chain: the per-bounce tails and gaps of the wavefront form (DESIGN.md
+// §7) are gone.  A shadow ray is any-hit with best initialised to tmax, which makes every bound of
+// the closest-hit loop the occlusion test's bound.
+#ifndef AKR_PATH_WAVES
+#define AKR_PATH_WAVES 4
+#endif
+
+// The traversal state of every lane is parked in LDS ([field][thread]) while the wave processes its
+// waiting lanes, so the shading code's registers are not stacked on top of it (128 VGPRs and ~80
+// spilled without this); the waiting lanes read their finished ray's result from the same place.
+constexpr int kParkFields = 12;  // o.xyz d.xyz tmin tmax best u v gid | cur | sp
+
+template <bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path(PathArgs pa) {
+    const TraceArgs &a = pa.t;
+    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ uint32_t s_park[kParkFields + 2][kTraceBlock];
+    lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
+    glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gtid = blockIdx.x * kTraceBlock + tid;
+    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
+    const uint32_t root = a.wide_root;
+    const float4 *wn = a.wide_nodes;
+    const uint32_t n = pa.n_pix;
+    const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
+    // COUNT: [0] closest-hit rays, [1] shadow rays
+    unsigned long long c_rays[2] = {0, 0}, c_box[2] = {0, 0}, c_tri[2] = {0, 0}, c_visit[2] = {0, 0}, c_deep[2] = {0, 0};
+    unsigned long long c_strav = 0, c_sleaf = 0, c_stri = 0;
+    bool deep = false;
+
+    // pixel fetch: kWorkShards contiguous ranges of the pixel list, one counter each (as k_trace)
+    uint32_t shard = blockIdx.x % kWorkShards;
+    int shards_left = kWorkShards;
+    uint32_t s_lo = shard_begin(n, shard), s_hi = shard_begin(n, shard + 1);
+    bool drained = n == 0;
+
+    // per-lane path state
+    uint32_t pix = 0, left = 0, seed = 0;
+    int depth = 0;
+    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f};
+    float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
+    bool pend = false;
+    bool any = false;           // the current ray is a shadow ray
+    bool need_pixel = true, done = false, fin = false;
+    // traversal state (k_trace); a shadow ray's hit is bgid != kNoHit
+    V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
+    float tmin = 0.0f, tmax = 0.0f, tmaxp = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
+    uint32_t dpos = 0, bgid = kNoHit, cur = AKR_CHILD_EMPTY, leaf = AKR_CHILD_EMPTY;
+    int sp = 0;
+    bool busy = false;
+    unsigned long long p_outer = 0, p_procs = 0, p_iters = 0, p_tp = 0, p_tt = 0, p_tl = 0, p_lanes = 0, p_t0 = 0, p_t = 0,
+                       p_tsh = 0;
+    if (COUNT) p_t0 = wall_clock64();
+
+    while (true) {
+        // ---- A. lanes without a ray in flight
+        const unsigned long long waiting = __ballot(!busy && !done);
+        const uint32_t nwait = (uint32_t)__popcll(waiting);
+        const uint32_t nbusy = (uint32_t)__popcll(__ballot(busy));
+        if (nwait == 0 && nbusy == 0) break;
+        if (COUNT) {
+            p_outer++;
+            p_t = wall_clock64();
+        }
+        if (nwait > 0 && (nwait >= pa.min_wait || 2 * nwait >= nwait + nbusy)) {
+            if (COUNT) {
+                p_procs++;
+                p_lanes += nwait;
+            }
+            {   // park
+                const float pv[kParkFields] = {o.x, o.y, o.z, d.x, d.y, d.z, tmin, tmax, best, bu, bv, bitsf(bgid)};
+#pragma unroll
+                for (int k = 0; k < kParkFields; k++) s_park[k][tid] = fbits(pv[k]);
+                s_park[kParkFields][tid] = cur;
+                s_park[kParkFields + 1][tid] = (uint32_t)sp;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            asm volatile("" ::: "memory");
+            bool fresh = false, next_any = false, sample_end = false, start = false;
+            float4 ra = {}, rb = {};
+            unsigned long long p_ts = 0;
+            if (COUNT) p_ts = wall_clock64();
+            if (!busy && !done && fin) {
+                fin = false;
+                const uint32_t hgid = s_park[11][tid];
+                if (any) {  // shadow ray: NEE contribution when unoccluded (pathtracer.h:84-88)
+                    if (hgid == kNoHit) {
+                        Lr.x += scol.x;
+                        Lr.y += scol.y;
+                        Lr.z += scol.z;
+                    }
+                    if (pend) {
+                        ra = pe0;
+                        rb = pe1;
+                        fresh = true;
+                        pend = false;
+                    } else {
+                        sample_end = true;
+                    }
+                } else if (hgid == kNoHit) {  // on_miss: the sample ends
+                    sample_end = true;
+                } else {
+                    const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
+                    Bounce bo;
+#ifdef AKR_PROBE_NOSHADE
+                    bo.emit = false; bo.sh = false; bo.ext = hgid & 1; bo.e0 = make_float4(wo.x, wo.y, wo.z, 1.f); bo.e1 = bo.e0; bo.nb = wo;
+#else
+#ifdef AKR_PATH_INLINE_SHADE
+                    shade_hit(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
+                              pa.max_depth, depth == nb - 1, bo);
+#else
+                    shade_hit_call(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
+                                   pa.max_depth, depth == nb - 1, bo);
+#endif
+#endif
+                    if (bo.emit) {
+                        Lr.x += bo.e.x;
+                        Lr.y += bo.e.y;
+                        Lr.z += bo.e.z;
+                    }
+                    if (bo.ext) {
+                        beta = bo.nb;
+                        depth++;
+                    }
+                    if (bo.sh) {
+                        ra = bo.s0;
+                        rb = bo.s1;
+                        scol = bo.col;
+                        next_any = true;
+                        fresh = true;
+                        pend = bo.ext;
+                        pe0 = bo.e0;
+                        pe1 = bo.e1;
+                    } else if (bo.ext) {
+                        ra = bo.e0;
+                        rb = bo.e1;
+                        fresh = true;
+                    } else {
+                        sample_end = true;
+                    }
+                }
+            }
+            if (COUNT) p_tsh += wall_clock64() - p_ts;
+            if (sample_end) {  // Tile::add_sample (core/film.h:66-70), in sample order
+                splat_one(film, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
+                if (--left == 0) {
+                    pa.film[pix] = film;
+                    need_pixel = true;
+                } else {
+                    start = true;
+                }
+            }
+            // next pixel for the lanes that finished theirs: one atomic per wave per attempt
+            while (true) {
+                const unsigned long long want = __ballot(need_pixel && !done);
+                if (want == 0) break;
+                if (drained) {
+                    if (need_pixel) done = true;
+                    break;
+                }
+                const uint32_t nw = (uint32_t)__popcll(want);
+                const int leader = __ffsll((long long)want) - 1;
+                uint32_t base = 0;
+                if ((int)__lane_id() == leader) base = atomicAdd(pa.work + shard * kWorkStride, nw);
+                base = __shfl(base, leader);
+                if (need_pixel && !done) {
+                    const uint32_t my = s_lo + base + lane_prefix(want);
+                    if (base < s_hi - s_lo && my < s_hi) {
+                        pix = my;
+                        left = pa.spp;
+                        const uint32_t px = pa.pixel[pix];
+                        seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                        film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        need_pixel = false;
+                        start = true;
+                    }
+                }
+                if (base + nw >= s_hi - s_lo) {  // this shard is exhausted: move to the next open one
+                    while (true) {
+                        if (--shards_left == 0) {
+                            drained = true;
+                            break;
+                        }
+                        shard = (shard + 1) % kWorkShards;
+                        s_lo = shard_begin(n, shard);
+                        s_hi = shard_begin(n, shard + 1);
+                        const uint32_t taken = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                            pa.work + shard * kWorkStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (taken < s_hi - s_lo) break;
+                    }
+                }
+            }
+            if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
+                Lr = V3{0.0f, 0.0f, 0.0f};
+                beta = V3{1.0f, 1.0f, 1.0f};
+                depth = 0;
+                const uint32_t px = pa.pixel[pix];
+                camera_ray(pa.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, ra, rb);
+                fresh = true;
+            }
+            asm volatile("" ::: "memory");
+            {   // unpark (the busy lanes' traversal continues unchanged)
+                o = V3{bitsf(s_park[0][tid]), bitsf(s_park[1][tid]), bitsf(s_park[2][tid])};
+                d = V3{bitsf(s_park[3][tid]), bitsf(s_park[4][tid]), bitsf(s_park[5][tid])};
+                tmin = bitsf(s_park[6][tid]);
+                tmax = bitsf(s_park[7][tid]);
+                best = bitsf(s_park[8][tid]);
+                bu = bitsf(s_park[9][tid]);
+                bv = bitsf(s_park[10][tid]);
+                bgid = s_park[11][tid];
+                cur = s_park[kParkFields][tid];
+                sp = (int)s_park[kParkFields + 1][tid];
+                invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
+                if (any && a.any_far_first) dpos ^= 7u;
+                tmaxp = float_below(tmax);
+            }
+            if (fresh) {
+                any = next_any;
+                o = V3{ra.x, ra.y, ra.z};
+                d = V3{rb.x, rb.y, rb.z};
+                tmin = ra.w;
+                tmax = rb.w;
+                invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
+                if (any && a.any_far_first) dpos ^= 7u;
+                tmaxp = float_below(tmax);
+                if (COUNT) c_rays[any]++;
+                if (!lean_ok(o, invd, tmin, tmax)) {
+                    // rare: exact BVH2 walk inline (k_trace's exact lane)
+                    bool occ;
+                    if (any)
+                        trace_exact_core<true, true>(a, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid, best, bu, bv,
+                                                     bgid, occ);
+                    else
+                        trace_exact_core<false, true>(a, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid, best, bu, bv,
+                                                      bgid, occ);
+                    fin = true;
+                } else {
+                    best = any ? tmax : kInf;
+                    bu = bv = 0.0f;
+                    bgid = kNoHit;
+                    sp = 0;
+                    leaf = AKR_CHILD_EMPTY;
+                    if (COUNT) {
+                        c_box[any]++;
+                        deep = false;
+                    }
+                    const float4 r0 = nodesf[0], r2 = nodesf[2];
+                    const float tr = box_test<true, true>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
+                    cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > best) ? AKR_CHILD_EMPTY : root;
+                    busy = true;
+                }
+            }
+        }
+        if (COUNT) {
+            const unsigned long long t = wall_clock64();
+            p_tp += t - p_t;
+            p_t = t;
+        }
+        if (!__any(busy)) continue;
+        // ---- B. traversal phase (k_trace; every ray here is lean)
+        while (true) {
+            if (COUNT) {
+                c_strav++;
+                c_sleaf += busy ? 1 : 0;
+                p_iters++;
+            }
+            if (busy && is_internal(cur)) {
+                const int nt = visit_wide_lean<false>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
+                                                      a.ovf_threads, tid, gtid, sp);
+                if (COUNT) {
+                    c_box[any] += nt;
+                    c_visit[any]++;
+                    deep = deep || sp > kStackLds;
+                }
+            }
+            if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
+                leaf = cur;  // postpone the leaf and keep descending
+                cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, best);
+            }
+            const unsigned long long searching = __ballot(busy && leaf == AKR_CHILD_EMPTY && cur != AKR_CHILD_EMPTY);
+            if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+                (searching == 0 || __ballot(busy && leaf != AKR_CHILD_EMPTY) != 0))
+                break;
+        }
+        if (COUNT) {
+            const unsigned long long t = wall_clock64();
+            p_tt += t - p_t;
+            p_t = t;
+        }
+        // ---- C. leaf phase: the leaf's exact box with the current best, then its triangles
+        bool hit_any = false;
+        if (busy && leaf != AKR_CHILD_EMPTY) {
+            const float4 *lr = a.wide_leaves + (leaf & 0x7FFFFFFFu);
+            const float4 l0 = lr[0], l1 = lr[1];
+            const float4 pa0 = lr[2], pb0 = lr[3], pc0 = lr[4];
+            const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
+            const bool in = !(tl < 0.0f || tl > best);
+            if (COUNT) c_box[any]++;
+            const uint32_t cnt = in ? fbits(l1.w) : 0u;
+            const float4 *tp = lr + 2;
+            for (uint32_t k = 0; k < cnt; k++) {
+                if (COUNT && lane_prefix(__ballot(1)) == 0) c_stri += 64;
+                const float4 ta = k == 0 ? pa0 : tp[3 * k + 0];
+                const float4 tb = k == 0 ? pb0 : tp[3 * k + 1];
+                const float4 tc = k == 0 ? pc0 : tp[3 * k + 2];
+                if (COUNT) c_tri[any]++;
+                float t, u, v;
+                if (mt(o, d, tmin, tmax, ta, tb, tc, best, t, u, v)) {
+                    best = t;
+                    bu = u;
+                    bv = v;
+                    bgid = fbits(ta.w);
+                    if (any) {
+                        hit_any = true;
+                        break;
+                    }
+                }
+            }
+            leaf = AKR_CHILD_EMPTY;
+        }
+        if (busy && (hit_any || cur == AKR_CHILD_EMPTY)) {
+            busy = false;
+            fin = true;
+            if (COUNT) c_deep[any] += deep ? 1 : 0;
+        }
+        if (COUNT) p_tl += wall_clock64() - p_t;
+    }
+    if (COUNT) {
+        if (__lane_id() == 0 && pa.prof) {
+            const unsigned long long tot = wall_clock64() - p_t0;
+            PathProfile &q = *pa.prof;
+            atomicAdd(&q.waves, 1ull);
+            atomicAdd(&q.outer, p_outer);
+            atomicAdd(&q.procs, p_procs);
+            atomicAdd(&q.trav_iters, p_iters);
+            atomicAdd(&q.t_proc, p_tp);
+            atomicAdd(&q.t_trav, p_tt);
+            atomicAdd(&q.t_leaf, p_tl);
+            atomicAdd(&q.t_total, tot);
+            atomicMax(&q.t_max, tot);
+            atomicAdd(&q.lanes_proc, p_lanes);
+            atomicAdd(&q.t_shade, p_tsh);
+        }
+        const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
+        for (int m = 0; m < 2; m++) {
+            const unsigned long long r = wave_sum(c_rays[m]), b = wave_sum(c_box[m]), t = wave_sum(c_tri[m]),
+                                     v = wave_sum(c_visit[m]), dp = wave_sum(c_deep[m]);
+            if (__lane_id() == 0) {
+                TraceCounters &tc = a.counters[slot_of[m]];
+                atomicAdd(&tc.rays, r);
+                atomicAdd(&tc.box, b);
+                atomicAdd(&tc.tri, t);
+                atomicAdd(&tc.visits, v);
+                atomicAdd(&tc.deep, dp);
+            }
+        }
+        c_strav = wave_sum(c_strav);
+        c_sleaf = wave_sum(c_sleaf);
+        c_stri = wave_sum(c_stri);
+        if (__lane_id() == 0) {  // lane-slot utilisation of the shared loop: under the closest-hit set
+            atomicAdd(&a.counters[TRACE_CLOSEST].slots_trav, c_strav);
+            atomicAdd(&a.counters[TRACE_CLOSEST].slots_leaf, c_sleaf);
+            atomicAdd(&a.counters[TRACE_CLOSEST].slots_tri, c_stri);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint32_t n, float *rad, float *w) {
@@ -1386,6 +1806,16 @@ void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t s
 void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_splat, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+}
+void launch_path(bool count, const PathArgs &a, uint32_t grid, hipStream_t st) {
+    if (grid == 0) return;
+    if (count) hipLaunchKernelGGL(k_path<true>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+    else hipLaunchKernelGGL(k_path<false>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+}
+int path_blocks_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false>, kTraceBlock, 0) != hipSuccess || nb <= 0) nb = 1;
+    return nb;
 }
 void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad, hipStream_t st) {
     if (n == 0) return;

@@ -34,6 +34,7 @@ RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic byte
 
 
 TRACE_KERNEL_PROF_NAME = "k_trace<0, false, true, true>"   # closest hit, uncounted, tight cull, wide (rocprof name)
+PATH_KERNEL_PROF_NAME = "k_path<false>"                      # persistent path kernel, uncounted
 
 
 def log(*a):
@@ -180,6 +181,8 @@ def main():
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
     ap.add_argument("--lean", type=int, default=1, help="lean slot tests in the wide traversal (0: reference arithmetic)")
+    ap.add_argument("--path", type=int, default=1,
+                    help="1: the persistent path kernel (one launch per render); 0: the wavefront kernels")
     ap.add_argument("--shadow-grid-pct", type=int, default=100, help="tuning: shadow-trace grid, %% of resident max")
     ap.add_argument("--timed-stats", type=int, default=-1,
                     help="HIP events inside the timed region: 2 = the dominant kernel (trace_closest) only, "
@@ -237,6 +240,7 @@ def main():
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)
+    ctx.set_option("path", args.path)
     if not args.lean:
         ctx.set_option("lean", 0)
     ctx.set_option("lookahead", args.lookahead)
@@ -322,21 +326,28 @@ def main():
         return
     samples = W * H * K
     value = samples / elapsed / 1e6
-    # roofline of the dominant kernel (closest-hit traversal)
+    # roofline of the dominant kernel: the persistent path kernel (every closest-hit and shadow ray
+    # of the render, SURVEY.md §8d "t_traversal_kernels"), or the wavefront's closest-hit trace
     cl = counts["per_mode"]["closest"]
-    n_cl_launch = cstats.get("trace_closest", {}).get("launches", 0) or 1
-    bytes_per_launch = (RAY_BYTES * cl["rays"] + BOX_BYTES * cl["box_tests"] + TRI_BYTES * cl["tri_tests"]) / n_cl_launch
-    kc = kstats.get("trace_closest") or bstats["trace_closest"]   # timed region (breakdown pass if --timed-stats 0)
+    sh = counts["per_mode"]["shadow"]
+    ray_bytes = lambda c: RAY_BYTES * c["rays"] + BOX_BYTES * c["box_tests"] + TRI_BYTES * c["tri_tests"]
+    dom = "path" if "path" in cstats else "trace_closest"
+    if dom == "path":   # the counting pass rendered 1 spp; the timed launch renders K
+        bytes_per_launch = (ray_bytes(cl) + ray_bytes(sh)) * K
+        prof_name = PATH_KERNEL_PROF_NAME
+    else:
+        bytes_per_launch = ray_bytes(cl) / (cstats.get("trace_closest", {}).get("launches", 0) or 1)
+        prof_name = TRACE_KERNEL_PROF_NAME
+    kc = kstats.get(dom) or bstats[dom]   # timed region (breakdown pass if --timed-stats 0)
     avg_ms = kc["total_ms"] / kc["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    sh = counts["per_mode"]["shadow"]
-    traffic, traffic_src = measured_traffic(TRACE_KERNEL_PROF_NAME, {
+    traffic, traffic_src = measured_traffic(prof_name, {
         "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf,
-        "sah_isect": args.sah_isect, "builder": args.builder})
+        "sah_isect": args.sah_isect, "builder": args.builder, "spp": K if dom == "path" else None})
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
-                "kernel": "trace_closest", "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
+                "kernel": dom, "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
                 "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
                             "node_visits": cl["visits"] / max(1, cl["rays"]),
                             "tri_tests": cl["tri_tests"] / max(1, cl["rays"])},

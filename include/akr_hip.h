@@ -252,6 +252,13 @@ const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h);
 
 int akr_hip_kernel_stats(akr_hip_ctx *ctx, akr_kernel_stat *out, int32_t max_n, int32_t *n);
 int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
+
+/* Diagnostic (option count_tests): phase profile of the persistent path kernel's last counted
+ * launches, summed over waves, wall-clock ticks at 100 MHz: out[0..10] = waves, outer iterations,
+ * processing phases, traversal-loop iterations, ticks processing / traversing / in leaves / in
+ * total, the longest wave's ticks, lanes processed, ticks of processing spent on finished rays'
+ * results (shading).  Not part of the reference interface. */
+int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
 /* The last akr_hip_render's lookahead lanes per pixel and sample passes launched (diagnostic). */
 int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);

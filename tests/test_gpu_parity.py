@@ -425,19 +425,46 @@ def test_trace_small_batches_and_grazing(hip_ctx_factory):
 
 
 def test_kernel_stats_modes(hip_ctx_factory):
-    """"stats" 1 times every kernel, 2 only trace_closest (bench.py's timed region at a split);
-    the image does not depend on it."""
+    """"stats" 1 times every kernel, 2 only the dominant one (bench.py's timed region at a split):
+    trace_closest in the wavefront form, the one persistent launch in the path-kernel form; the
+    image does not depend on either."""
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, cornell((32, 32)))
         ref, _ = ctx.render(3, 5, [(0, 0, 32, 32)], 32, 32)
-        for mode, expect in ((1, {"raygen", "trace_closest", "shade", "trace_shadow", "splat"}), (2, {"trace_closest"})):
+        cases = ((0, 1, {"raygen", "trace_closest", "shade", "trace_shadow", "splat"}, "trace_closest", 15),
+                 (0, 2, {"trace_closest"}, "trace_closest", 15), (1, 1, {"path"}, "path", 1), (1, 2, {"path"}, "path", 1))
+        for path, mode, expect, key, launches in cases:
+            ctx.set_option("path", path)
             ctx.reset_stats()
             ctx.set_option("stats", mode)
             rad, _ = ctx.render(3, 5, [(0, 0, 32, 32)], 32, 32)
             assert np.array_equal(rad, ref)
             ks = ctx.kernel_stats()
-            assert set(ks) == expect and ks["trace_closest"]["launches"] == 15
+            assert set(ks) == expect and ks[key]["launches"] == launches
         ctx.set_option("stats", 0)
+        ctx.set_option("path", 1)
+
+
+@pytest.mark.parametrize("path", [0, 1])
+def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path):
+    """The persistent path kernel (k_path) and the wavefront kernels give the
+    oracle's image bit for bit: ragged / clipped / empty tiles, depths 0-5, the clamp, Glossy + Mix
+    + two-sided emitter, image textures, a soup whose rays take the deep stack, and a tile list
+    smaller than one workgroup (fewer pixels than lanes)."""
+    with hip_ctx_factory(0) as ctx:
+        ctx.set_option("path", path)
+        cs, orc = _setup(ctx, cornell((40, 24)))
+        tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]
+        for spp, depth in ((3, 0), (2, 1), (3, 2), (5, 5)):
+            _check_render(ctx, orc, spp, depth, tiles, 40, 24)
+        _check_render(ctx, orc, 4, 5, tiles, 40, 24, clamp=10.0)
+        _check_render(ctx, orc, 7, 5, [(3, 3, 10, 8)], 40, 24)
+    for sc in (mixed_scene((48, 48)), textured_scene((40, 40)), small_soup(100_000, (64, 36))):
+        with hip_ctx_factory(0) as ctx:   # one scene per context (uploads append meshes)
+            ctx.set_option("path", path)
+            cs, orc = _setup(ctx, sc)
+            W, H = cs.camera.resolution
+            _check_render(ctx, orc, 5, 5, [(0, 0, W, H)], W, H)
 
 
 @pytest.mark.parametrize("spp", [16, 32])

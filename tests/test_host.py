@@ -510,3 +510,19 @@ def test_lean_slot_test_conservative_on_grid_bounds():
         checked += int(rh.sum())
     assert checked > 30_000
     assert bad == 0
+
+
+def test_device_trig_matches_libm_on_path_range(tmp_path):
+    """The device's fsin/fcos (akr_trig.h: fdlibm-style f64 reduction and kernels) against the C
+    library's f64 sin/cos that the oracle uses, both rounded to f32, on every 64th f32 in
+    [-2 pi, 2 pi] (the path's arguments: concentric_disk theta, GGX phi).  Run with stride 1 it covers
+    all 2.17e9 inputs; that exhaustive run found no difference."""
+    import subprocess
+    exe = tmp_path / "trig_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread",
+                    f"-I{ROOT / 'akarirender-1_amd' / 'csrc'}", str(ROOT / "tests" / "cpp" / "trig_check.cpp"),
+                    "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "64", "8"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    n, bad = (int(v) for v in re.findall(r"\d+", out.stdout))
+    assert n > 30_000_000 and bad == 0

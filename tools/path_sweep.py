@@ -1,0 +1,101 @@
+"""Tuning sweep of the persistent path kernel (k_path) on C3: per library build (AKR_HIP_LIB variants
+or the product lib) and per runtime setting, the full-frame step (N = 1) and the step of one rank's
+share of an 8-way tile split.  One scene generation per process, one BVH build per library.
+
+Usage (GPU box): python tools/path_sweep.py [--libs a.so,b.so] [--min-wait 16,32,48] [--steps 8]"""
+import argparse
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "akarirender-1_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default=str(ROOT / "akarirender-1_amd" / "libakr_hip.so"))
+    ap.add_argument("--min-wait", default="32")
+    ap.add_argument("--path", default="1")
+    ap.add_argument("--far-first", default="1", help="occlusion rays far slots first (comma list)")
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--tris", type=int, default=10_000_000)
+    ap.add_argument("--builder", default="sbvh")
+    ap.add_argument("--profile", type=int, default=0, help="also print the counted k_path phase profile")
+    args = ap.parse_args()
+    libs = args.libs.split(",")
+    if len(libs) > 1:
+        # one child process per library: the product binding loads the library RTLD_GLOBAL, so a
+        # second library in the same process would have its internal calls bound to the first one's
+        # kernels.  This parent never touches the GPU.
+        import subprocess
+        rc = 0
+        for lib in libs:
+            argv = [a for a in sys.argv[1:]]
+            k = argv.index("--libs")
+            argv[k + 1] = lib
+            rc = rc or subprocess.run([sys.executable, "-u", __file__, *argv]).returncode
+        sys.exit(rc)
+    import torch
+    from akari_amd import dist
+    dev = torch.device("cuda", 0)
+    W, H = 1920, 1080
+    full = dist.tile_grid(W, H, 32)
+    share = dist.tiles_for_rank(W, H, 32, 0, 8)
+    film = torch.zeros(4 * W * H, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for lib in libs:
+        os.environ["AKR_HIP_LIB"] = lib
+        import akari_amd.capi as capi
+        import akari_amd.scene as scene
+        cs = scene.compile_scene(scene.soup_scene(n_tris=args.tris, resolution=(W, H)))  # this module's types
+        ctx = capi.HipContext(0)
+        t0 = time.time()
+        scene.upload_scene(ctx, cs, builder={"sah": capi.BUILDER_SAH, "sbvh": capi.BUILDER_SBVH,
+                                             "lbvh": capi.BUILDER_LBVH}[args.builder], n_threads=16)
+        print(f"== {Path(lib).name}: built in {time.time() - t0:.1f} s", flush=True)
+        combos = [(p, f) for p in (int(x) for x in args.path.split(",")) for f in (int(x) for x in args.far_first.split(","))]
+        for path, ff in combos:
+            ctx.set_option("path", path)
+            ctx.set_option("any_far_first", ff)
+            for mw in (int(x) for x in args.min_wait.split(",")):
+                ctx.set_option("path_min_wait", mw)
+                res = []
+                for tiles in (full, share):
+                    n = dist.n_pixels(tiles)
+                    ctx.render_device(2, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
+                    torch.cuda.synchronize(dev)
+                    t = time.perf_counter()
+                    ctx.render_device(args.steps, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
+                    torch.cuda.synchronize(dev)
+                    res.append((time.perf_counter() - t) / args.steps * 1e3)
+                print(f"   path={path} far_first={ff} min_wait={mw}: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s), "
+                      f"8-way rank {res[1]:.3f} ms/step (projected {res[0] / res[1]:.2f}x)", flush=True)
+                if args.profile and path:
+                    for name, tiles in (("full", full), ("8-way", share)):
+                        n = dist.n_pixels(tiles)
+                        ctx.set_option("count_tests", 1)
+                        ctx.reset_stats()
+                        ctx.render_device(args.steps, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
+                        torch.cuda.synchronize(dev)
+                        q = ctx.path_profile()
+                        c = ctx.trace_counts()
+                        ctx.set_option("count_tests", 0)
+                        w = max(1, q["waves"])
+                        us = lambda t: t / 100.0   # 100 MHz ticks -> us
+                        print(f"     {name} counted: waves {q['waves']}, mean wave {us(q['t_total'] / w):.0f} us, longest "
+                              f"{us(q['t_max']):.0f} us; per wave: outer {q['outer'] / w:.0f}, proc {q['procs'] / w:.0f} "
+                              f"({q['lanes_proc'] / max(1, q['procs']):.1f} lanes each), trav iters {q['trav_iters'] / w:.0f}; "
+                              f"time proc {q['t_proc'] / max(1, q['t_total']):.3f} trav {q['t_trav'] / max(1, q['t_total']):.3f} "
+                              f"leaf {q['t_leaf'] / max(1, q['t_total']):.3f}; us per trav iter "
+                              f"{us(q['t_trav']) / max(1, q['trav_iters']):.3f}, per proc {us(q['t_proc']) / max(1, q['procs']):.2f} "
+                              f"(results/shading {us(q['t_shade']) / max(1, q['procs']):.2f}), "
+                              f"per outer leaf {us(q['t_leaf']) / max(1, q['outer']):.3f}; rays/px closest "
+                              f"{c['per_mode']['closest']['rays'] / n / args.steps:.2f} shadow "
+                              f"{c['per_mode']['shadow']['rays'] / n / args.steps:.2f}", flush=True)
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()
