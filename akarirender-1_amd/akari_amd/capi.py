@@ -129,6 +129,7 @@ EXPORTS = {
                                         C.POINTER(C.c_uint64)]),
     "akr_hip_kernel_stats": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "akr_hip_trace_counts": (C.c_int, [_P, C.POINTER(TraceCounts)]),
+    "akr_hip_path_profile": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int32]),
     "akr_hip_reset_stats": (C.c_int, [_P]),
     "akr_hip_render_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "akr_hip_synchronize": (C.c_int, [_P]),
@@ -397,6 +398,14 @@ class HipContext:
         lanes, passes = C.c_int32(0), C.c_int32(0)
         self._check(self.lib.akr_hip_render_info(self.h, C.byref(lanes), C.byref(passes)))
         return {"lanes": lanes.value, "passes": passes.value}
+
+    def path_profile(self) -> dict:
+        """k_path phase profile of the counted launches since reset_stats (ticks: 100 MHz)."""
+        out = (C.c_uint64 * 11)()
+        self._check(self.lib.akr_hip_path_profile(self.h, out, 11))
+        keys = ("waves", "outer", "procs", "trav_iters", "t_proc", "t_trav", "t_leaf", "t_total", "t_max", "lanes_proc",
+                "t_shade")
+        return dict(zip(keys, (int(v) for v in out)))
 
     def trace_counts(self) -> dict:
         c = TraceCounts()
