@@ -9,6 +9,7 @@
 //           slot u32 — path state travels with the ray, so shade reads and writes it coalesced;
 //           hits float4 (t, u, v, gid bits); shadow queue ray float4[2] + (colour|slot) float4
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 #include "../../include/akr_hip.h"
@@ -56,12 +57,31 @@ __host__ __device__ inline uint32_t shard_begin(uint32_t n, uint32_t k) {
     return (uint32_t)(((uint64_t)n * k) / kWorkShards);
 }
 
-struct LightDev {          // AreaLight (kernel/light.h:47-57): triangle + emission texture
-    float v[9];
-    float tc[6];
-    int32_t color_tex;
-    int32_t _pad[2];
+// AreaLight (kernel/light.h:47-71): triangle, texcoords, emission, and the per-light constants of
+// AreaLight::sample / Scene::select_light precomputed on the host with the device's f32 operations
+// (cross, normalize, length, one division): one 96-B record per NEE sample, no dependent loads.
+struct LightDev {
+    float v[9];            // corners
+    float tc[6];           // corner texcoords
+    int32_t color_img;     // -1: constant emission Le; else the (image) texture index
+    float Le[3];           // constant emission
+    float area_half;       // length(cross(v1 - v0, v2 - v0)) * 0.5
+    float lng[3];          // normalize(cross(v1 - v0, v2 - v0))
+    float sel_pdf;         // light_func[i] / (light_func_int * n_lights) (scene.h:79-90)
 };
+
+// akr_material with its constant textures resolved (Texture::evaluate of a ConstantTexture is its
+// value): one 48-B record per material lookup; *_img >= 0 names an image texture to evaluate.
+struct MatDev {
+    int32_t type, double_sided, first, second;
+    float color[3];
+    int32_t color_img;
+    float rough;
+    int32_t rough_img;
+    float frac;
+    int32_t frac_img;
+};
+static_assert(sizeof(LightDev) == 96, "LightDev: six float4");
 
 struct ShadeTri {          // Triangle<C> data of one global triangle id (shape.h:26-42)
     float4 a;              // v0.xyz, material id (int bits, -1 = none)
@@ -84,13 +104,11 @@ struct SceneDev {
     const ShadeTri *tri;           // per global triangle id
     const float *texcoords;        // 6 per triangle (read only when has_image_tex)
     int32_t has_image_tex;
-    const akr_material *mats;
+    const MatDev *mats;
     const TexDev *texs;
     const float *images;
     const LightDev *lights;
     const float *light_cdf;        // n_lights + 1
-    const float *light_func;       // n_lights
-    float light_func_int;
     int32_t n_lights;
 };
 

@@ -189,7 +189,7 @@ struct akr_hip_ctx {
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
-    DBuf<akr_material> d_mats;
+    DBuf<MatDev> d_mats;
     DBuf<TexDev> d_texs;
     DBuf<LightDev> d_lights;
     DBuf<uint32_t> d_mesh_base;
@@ -234,7 +234,11 @@ struct akr_hip_ctx {
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     uint32_t path_grid = 0;   // resident workgroups of the persistent path kernel
-    bool path_kernel = true;  // option "path": render with k_path (false: the wavefront kernels)
+    // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the
+    // render has at most path_auto_pixels pixels (measured on C3, DESIGN.md §3.8: the wavefront is ~6 %
+    // faster on a whole 1080p frame, k_path 10-33 % faster on a 2-, 4- or 8-way share)
+    int path_kernel = 2;
+    int64_t path_auto_pixels = 1500000;
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
     int path_min_wait = 32;   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
     DBuf<float4> d_trace_rays;
@@ -333,8 +337,6 @@ struct akr_hip_ctx {
         s.images = d_images.p;
         s.lights = d_lights.p;
         s.light_cdf = d_cdf.p;
-        s.light_func = d_func.p;
-        s.light_func_int = func_int;
         s.n_lights = n_lights;
         return s;
     }
@@ -381,7 +383,29 @@ struct akr_hip_ctx {
         }
         d_shade_tri.upload(st.data(), st.size(), stream);
         if (has_image_tex) d_tc.upload(texcoords.data(), texcoords.size(), stream);
-        d_mats.upload(mats.data(), mats.size(), stream);
+        // materials with constant textures resolved (MatDev)
+        std::vector<MatDev> md(mats.size());
+        for (size_t m = 0; m < mats.size(); m++) {
+            const akr_material &x = mats[m];
+            MatDev &d = md[m];
+            std::memset(&d, 0, sizeof(d));
+            d.type = x.type;
+            d.double_sided = x.double_sided;
+            d.first = x.first;
+            d.second = x.second;
+            d.color_img = d.rough_img = d.frac_img = -1;
+            auto resolve = [&](int32_t ti, float *val, int n, int32_t &img) {
+                if (ti < 0 || ti >= (int32_t)texs.size()) return;  // unused by this material type
+                if (texs[ti].type == AKR_TEX_IMAGE) img = ti;
+                else
+                    for (int c = 0; c < n; c++) val[c] = texs[ti].value[c];
+            };
+            if (x.type == AKR_MAT_DIFFUSE || x.type == AKR_MAT_EMISSIVE || x.type == AKR_MAT_GLOSSY)
+                resolve(x.color, d.color, 3, d.color_img);
+            if (x.type == AKR_MAT_GLOSSY) resolve(x.roughness, &d.rough, 1, d.rough_img);
+            if (x.type == AKR_MAT_MIX) resolve(x.fraction, &d.frac, 1, d.frac_img);
+        }
+        d_mats.upload(md.data(), md.size(), stream);
         std::vector<TexDev> td(texs.size());
         for (size_t k = 0; k < texs.size(); k++) {
             const akr_texture &t = texs[k];
@@ -416,7 +440,22 @@ struct akr_hip_ctx {
                 x.tc[2 * k + 0] = texcoords[6 * g + 2 * k + 0];
                 x.tc[2 * k + 1] = texcoords[6 * g + 2 * k + 1];
             }
-            x.color_tex = mats[m].color;
+            const akr_texture &lt = texs[mats[m].color];
+            x.color_img = lt.type == AKR_TEX_IMAGE ? mats[m].color : -1;
+            for (int c = 0; c < 3; c++) x.Le[c] = lt.type == AKR_TEX_IMAGE ? 0.0f : lt.value[c];
+            // AreaLight::sample's triangle constants (light.h:58-71), in the device's f32 order:
+            // lx = cross(v1 - v0, v2 - v0) (math.h:176-181), lng = lx / sqrt(dot(lx, lx)),
+            // area_half = sqrt(dot(lx, lx)) * 0.5
+            const float e1[3] = {x.v[3] - x.v[0], x.v[4] - x.v[1], x.v[5] - x.v[2]};
+            const float e2[3] = {x.v[6] - x.v[0], x.v[7] - x.v[1], x.v[8] - x.v[2]};
+            const float lx[3] = {(e1[1] * e2[2]) - (e1[2] * e2[1]), (e1[2] * e2[0]) - (e1[0] * e2[2]),
+                                 (e1[0] * e2[1]) - (e1[1] * e2[0])};
+            float dd = lx[0] * lx[0];
+            dd += lx[1] * lx[1];
+            dd += lx[2] * lx[2];
+            const float len = std::sqrt(dd);
+            for (int c = 0; c < 3; c++) x.lng[c] = lx[c] / len;
+            x.area_half = len * 0.5f;
             ld.push_back(x);
         }
         n_lights = (int32_t)ld.size();
@@ -429,9 +468,9 @@ struct akr_hip_ctx {
         } else {
             for (uint32_t i = 1; i < n + 1; ++i) cdf[i] /= func_int;
         }
+        for (size_t i = 0; i < n; i++) ld[i].sel_pdf = func[i] / (func_int * (float)n_lights);  // scene.h:85-89
         d_lights.upload(ld.data(), ld.size(), stream);
         d_cdf.upload(cdf.data(), cdf.size(), stream);
-        d_func.upload(func.data(), func.size(), stream);
         HIPCHK(hipStreamSynchronize(stream));
         scene_dirty = false;
     }
@@ -728,7 +767,8 @@ struct akr_hip_ctx {
         // Persistent path kernel: every sample of every pixel in one launch.  It
         // runs the lean wide traversal only; the reference cull, the BVH2 kernel, a wide view whose
         // frames exceed the lean test's bounds and lookahead lanes keep the wavefront form.
-        if (path_kernel && tight && wide && !la && trace_args(nullptr).lean) {
+        const bool use_path = path_kernel == 1 || (path_kernel == 2 && (int64_t)N <= path_auto_pixels);
+        if (use_path && tight && wide && !la && trace_args(nullptr).lean) {
             if (p.spp > 0) {
                 HIPCHK(hipMemsetAsync(d_counts.p, 0, kWorkWords * sizeof(uint32_t), ms));
                 PathArgs pa{};
@@ -1009,7 +1049,11 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
                 throw std::runtime_error("lookahead must be in [0, 64] (0 = auto, 1 = off, n = on with at most n lanes)");
             ctx->lookahead = (int)value;
         } else if (k == "path") {
-            ctx->path_kernel = value != 0;
+            if (value < 0 || value > 2) throw std::runtime_error("path must be 0 (wavefront), 1 (path kernel) or 2 (auto)");
+            ctx->path_kernel = (int)value;
+        } else if (k == "path_auto_pixels") {
+            if (value < 0) throw std::runtime_error("path_auto_pixels must be >= 0");
+            ctx->path_auto_pixels = value;
         } else if (k == "any_far_first") {
             ctx->any_far_first = value != 0;
         } else if (k == "path_min_wait") {

@@ -1056,6 +1056,14 @@ struct Bounce {
     V3 col;
 };
 
+// Material channel: the resolved constant, or the image texture's texel
+__device__ __forceinline__ V3 mat_rgb(const SceneDev &s, const float (&c)[3], int32_t img, V2 tc) {
+    return img < 0 ? v3(c[0], c[1], c[2]) : tex_eval(s, img, tc);
+}
+__device__ __forceinline__ float mat_x(const SceneDev &s, float c, int32_t img, V2 tc) {
+    return img < 0 ? c : tex_eval(s, img, tc).x;
+}
+
 __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
                                           uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
     o.emit = o.ext = o.sh = false;
@@ -1067,18 +1075,18 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     const V3 p = lerp3(v0, v1, v2, u, v);
     const V3 ng = normalize(cross(sub(v1, v0), sub(v2, v0)));
     const V3 ns = lerp3(v3(tr.b.w, tr.c.w, tr.d.x), v3(tr.d.y, tr.d.z, tr.d.w), v3(tr.e.x, tr.e.y, tr.e.z), u, v);
-    V2 tc{0.0f, 0.0f};  // only textures read it; constant textures ignore it
+    V2 tc{0.0f, 0.0f};  // only image textures read it
     if (s.has_image_tex) {
         const float *tt = s.texcoords + 6 * (size_t)gid;
         tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
     }
-    const akr_material *mat = &s.mats[mid];
+    const MatDev *mat = &s.mats[mid];
     if (mat->type == AKR_MAT_EMISSIVE) {
         if (depth == 0) {
             const bool face_front = dot(neg(wo), ng) < 0.0f;
             if (mat->double_sided || face_front) {
                 o.emit = true;
-                o.e = mul(beta, tex_eval(s, mat->color, tc));
+                o.e = mul(beta, mat_rgb(s, mat->color, mat->color_img, tc));
             }
         }
         return;
@@ -1089,7 +1097,7 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     float sel_u = lcg_next(copy);
     float choice_pdf = 1.0f;
     while (mat->type == AKR_MAT_MIX) {  // Material::select_material, material.h:251-268
-        const float frac = tex_eval(s, mat->fraction, tc).x;
+        const float frac = mat_x(s, mat->frac, mat->frac_img, tc);
         if (sel_u < frac) {
             sel_u = sel_u / frac;
             mat = &s.mats[mat->second];
@@ -1103,11 +1111,11 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     Closure cl{CL_NONE, v3(0, 0, 0), 0.0f};
     if (mat->type == AKR_MAT_DIFFUSE) {
         cl.kind = CL_DIFFUSE;
-        cl.R = tex_eval(s, mat->color, tc);
+        cl.R = mat_rgb(s, mat->color, mat->color_img, tc);
     } else if (mat->type == AKR_MAT_GLOSSY) {
         cl.kind = CL_GLOSSY;
-        cl.R = tex_eval(s, mat->color, tc);
-        float r = tex_eval(s, mat->roughness, tc).x;
+        cl.R = mat_rgb(s, mat->color, mat->color_img, tc);
+        float r = mat_x(s, mat->rough, mat->rough_img, tc);
         r *= r;
         cl.alpha = r;
     }
@@ -1132,32 +1140,34 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
         }
         int li = hi - 1;
         li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
-        const float sel_pdf = s.light_func[li] / (s.light_func_int * (float)s.n_lights);
         const LightDev &lt = s.lights[li];
         const V2 lu = lcg_next2(seed);
-        // AreaLight::sample (light.h:58-71)
+        // AreaLight::sample (light.h:58-71); lng, the area and the selection pdf are precomputed
         const float su0 = sqrtf(lu.x);
         const float b0 = 1 - su0, b1 = lu.y * su0;
-        const V3 l0 = ld3(lt.v), l1 = ld3(lt.v + 3), l2 = ld3(lt.v + 6);
-        const V3 lp = lerp3(l0, l1, l2, b0, b1);
-        const V3 lx = cross(sub(l1, l0), sub(l2, l0));
-        const V3 lng = normalize(lx);
+        const V3 lp = lerp3(ld3(lt.v), ld3(lt.v + 3), ld3(lt.v + 6), b0, b1);
+        const V3 lng = ld3(lt.lng);
         V3 lwi = sub(lp, p);
         const float dist_sqr = dot(lwi, lwi);
         lwi = divs(lwi, sqrtf(dist_sqr));
-        const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]}, V2{lt.tc[4], lt.tc[5]}, b0, b1);
-        const V3 Le = tex_eval(s, lt.color_tex, ltc);
-        const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / (length(lx) * 0.5f);
+        V3 Le;
+        if (lt.color_img < 0) {
+            Le = ld3(lt.Le);
+        } else {
+            const V2 ltc = lerp3(V2{lt.tc[0], lt.tc[1]}, V2{lt.tc[2], lt.tc[3]}, V2{lt.tc[4], lt.tc[5]}, b0, b1);
+            Le = tex_eval(s, lt.color_img, ltc);
+        }
+        const float lpdf = dist_sqr / rmax(0.0f, -dot(lwi, lng)) / lt.area_half;
         if (!(lpdf <= 0.0f)) {
-            const float light_pdf = sel_pdf * lpdf;
+            const float light_pdf = lt.sel_pdf * lpdf;
             const V3 fe = closure_eval(cl, to_local(frame, wo), to_local(frame, lwi));
             const V3 fl = muls(mul(Le, fe), fabsf(dot(ns, lwi)));
             const V3 col = divs(mul(beta, fl), light_pdf);
             if (!is_black(col)) {
                 o.sh = true;
-                const V3 sd = neg(lwi);
+                const V3 sdir = neg(lwi);
                 o.s0 = make_float4(lp.x, lp.y, lp.z, kEps / fabsf(dot(lwi, lng)));
-                o.s1 = make_float4(sd.x, sd.y, sd.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
+                o.s1 = make_float4(sdir.x, sdir.y, sdir.z, sqrtf(dist_sqr) * (1.0f - kShadowEps));
                 o.col = col;
             }
         }

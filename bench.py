@@ -41,7 +41,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def measured_traffic(kernel, workload):
+def measured_traffic(kernel, workload, per_spp=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC profile of this same workload
     (profiles/<tag>_traffic.json, written by tools/prof_summary.py from separate FETCH_SIZE and
     WRITE_SIZE rocprofv3 passes, gfx950 FETCH_SIZE x2 correction).  PMC passes cannot run inside
@@ -56,7 +56,13 @@ def measured_traffic(kernel, workload):
         defaults = {"builder": "sah"}  # profiles written before the key existed
         if any(w.get(k, defaults.get(k)) != v for k, v in workload.items()) or kernel not in d.get("kernels", {}):
             continue
-        best = (d["kernels"][kernel]["hbm_bytes_per_launch"], f"profiles/{p.name}")
+        rec = d["kernels"][kernel]
+        if per_spp is not None:   # a persistent launch renders every spp: scale the profile's per-spp bytes
+            if "hbm_bytes_per_spp" not in rec:
+                continue
+            best = (rec["hbm_bytes_per_spp"] * per_spp, f"profiles/{p.name}")
+        else:
+            best = (rec["hbm_bytes_per_launch"], f"profiles/{p.name}")
     return best if best else (None, None)
 
 
@@ -154,7 +160,8 @@ def main():
                          "starts the ranks itself")
     ap.add_argument("--launch-check", action="store_true",
                     help="test the rank launch and the frame-end gather on CPU (gloo), no GPU work")
-    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=1024,
+                    help="spp of the timed render (default: the metric's 1024-spp frame, ~6 s at N = 1)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", choices=["soup", "cornell", "hall"], default="soup",
                     help="soup: C3, the headline workload; cornell: C2 (BASELINE.json configs[1], the reference's "
@@ -181,8 +188,9 @@ def main():
     ap.add_argument("--rays-per-lane", type=int, default=1, help="trace grid sizing (tuning)")
     ap.add_argument("--wide", type=int, default=1, help="4-wide quantized traversal (0: BVH2 kernel)")
     ap.add_argument("--lean", type=int, default=1, help="lean slot tests in the wide traversal (0: reference arithmetic)")
-    ap.add_argument("--path", type=int, default=1,
-                    help="1: the persistent path kernel (one launch per render); 0: the wavefront kernels")
+    ap.add_argument("--path", type=int, default=2,
+                    help="1: the persistent path kernel (one launch per render); 0: the wavefront kernels; "
+                         "2: the library's choice by the rank's pixel count (DESIGN.md §3.8)")
     ap.add_argument("--shadow-grid-pct", type=int, default=100, help="tuning: shadow-trace grid, %% of resident max")
     ap.add_argument("--timed-stats", type=int, default=-1,
                     help="HIP events inside the timed region: 2 = the dominant kernel (trace_closest) only, "
@@ -343,7 +351,7 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic, traffic_src = measured_traffic(prof_name, {
         "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf,
-        "sah_isect": args.sah_isect, "builder": args.builder, "spp": K if dom == "path" else None})
+        "sah_isect": args.sah_isect, "builder": args.builder}, per_spp=K if dom == "path" else None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
@@ -354,11 +362,16 @@ def main():
                 "shadow_per_ray": {"box_tests": sh["box_tests"] / max(1, sh["rays"]),
                                    "tri_tests": sh["tri_tests"] / max(1, sh["rays"])},
                 # SIMD lane utilisation of the traversal loop (node visits per lane slot) and of
-                # the triangle loop (triangle tests per lane slot), from the counting pass
-                "lane_util": {m: {"traversal": c["visits"] / max(1, c["slots_traversal"]),
-                                  "holding_ray": c["slots_busy"] / max(1, c["slots_traversal"]),
-                                  "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
-                              for m, c in (("closest", cl), ("shadow", sh))}}
+                # the triangle loop (triangle tests per lane slot), from the counting pass; the path
+                # kernel runs both ray kinds in one loop (its slots are counted with the closest set)
+                "lane_util": ({"path": {"traversal": (cl["visits"] + sh["visits"]) / max(1, cl["slots_traversal"]),
+                                        "holding_ray": cl["slots_busy"] / max(1, cl["slots_traversal"]),
+                                        "triangles": (cl["tri_tests"] + sh["tri_tests"]) / max(1, cl["slots_tri"])}}
+                              if dom == "path" else
+                              {m: {"traversal": c["visits"] / max(1, c["slots_traversal"]),
+                                   "holding_ray": c["slots_busy"] / max(1, c["slots_traversal"]),
+                                   "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
+                               for m, c in (("closest", cl), ("shadow", sh))})}
 
     cpu = None
     if args.cpu_baseline and world == 1:

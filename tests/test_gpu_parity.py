@@ -441,8 +441,15 @@ def test_kernel_stats_modes(hip_ctx_factory):
             assert np.array_equal(rad, ref)
             ks = ctx.kernel_stats()
             assert set(ks) == expect and ks[key]["launches"] == launches
+        # auto (the default): the path kernel up to path_auto_pixels pixels, the wavefront above
+        ctx.set_option("path", 2)
+        ctx.set_option("stats", 2)
+        for limit, key in ((1 << 20, "path"), (1000, "trace_closest")):
+            ctx.set_option("path_auto_pixels", limit)
+            ctx.reset_stats()
+            rad, _ = ctx.render(3, 5, [(0, 0, 32, 32)], 32, 32)
+            assert np.array_equal(rad, ref) and set(ctx.kernel_stats()) == {key}
         ctx.set_option("stats", 0)
-        ctx.set_option("path", 1)
 
 
 @pytest.mark.parametrize("path", [0, 1])

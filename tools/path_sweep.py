@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--builder", default="sbvh")
     ap.add_argument("--profile", type=int, default=0, help="also print the counted k_path phase profile")
+    ap.add_argument("--splits", default="8", help="emulated ranks of the tile split to time besides the full frame")
     args = ap.parse_args()
     libs = args.libs.split(",")
     if len(libs) > 1:
@@ -42,7 +43,9 @@ def main():
     dev = torch.device("cuda", 0)
     W, H = 1920, 1080
     full = dist.tile_grid(W, H, 32)
-    share = dist.tiles_for_rank(W, H, 32, 0, 8)
+    splits = [int(x) for x in args.splits.split(",")]
+    shares = {n: dist.tiles_for_rank(W, H, 32, 0, n) for n in splits}
+    share = shares[splits[-1]]
     film = torch.zeros(4 * W * H, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     for lib in libs:
@@ -62,7 +65,7 @@ def main():
             for mw in (int(x) for x in args.min_wait.split(",")):
                 ctx.set_option("path_min_wait", mw)
                 res = []
-                for tiles in (full, share):
+                for tiles in [full] + [shares[n] for n in splits]:
                     n = dist.n_pixels(tiles)
                     ctx.render_device(2, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
                     torch.cuda.synchronize(dev)
@@ -70,8 +73,9 @@ def main():
                     ctx.render_device(args.steps, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
                     torch.cuda.synchronize(dev)
                     res.append((time.perf_counter() - t) / args.steps * 1e3)
-                print(f"   path={path} far_first={ff} min_wait={mw}: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s), "
-                      f"8-way rank {res[1]:.3f} ms/step (projected {res[0] / res[1]:.2f}x)", flush=True)
+                print(f"   path={path} far_first={ff} min_wait={mw}: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
+                      + "".join(f", {n}-way rank {r:.3f} ms/step (projected {res[0] / r:.2f}x, {W * H / r / 1e3:.0f} Msamples/s)"
+                                for n, r in zip(splits, res[1:])), flush=True)
                 if args.profile and path:
                     for name, tiles in (("full", full), ("8-way", share)):
                         n = dist.n_pixels(tiles)
