@@ -243,6 +243,10 @@ struct akr_hip_ctx {
     int path_min_wait = 32;   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
     DBuf<float4> d_trace_rays;
     DBuf<akr_hit> d_trace_hits;
+    // akr_hip_render_node on the lead context: the frame and the staging of other contexts' films
+    DBuf<float> d_frame;
+    DBuf<float4> d_gfilm;
+    DBuf<uint32_t> d_gpix, d_gorder;
 
     // instrumentation
     bool stats = false, count = false;
@@ -1284,21 +1288,16 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
     // one host thread per context, each bound to its device by guard()
     std::vector<std::vector<akr_rect>> part(n_ctx);
     for (int32_t j = 0; j < n_tiles; j++) part[j % n_ctx].push_back(tiles[j]);
-    std::vector<std::vector<float4>> film(n_ctx);
-    std::vector<std::vector<uint32_t>> pix(n_ctx);
+    std::vector<uint64_t> npix(n_ctx, 0);
     std::vector<int> status(n_ctx, 0);
     run_on_threads(n_ctx, [&](int k) {
         akr_hip_ctx *c = ctxs[k];
         status[k] = guard(c, [&] {
             hipStream_t st = c->stream;
             const uint64_t N = c->render(*params, part[k].data(), (int32_t)part[k].size(), st);
-            film[k].resize(N);
-            if (N) c->host_join();  // see merge_film
-            c->verify_weights(st, N, params->spp);
-            if (N) HIPCHK(hipMemcpyAsync(film[k].data(), c->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
+            c->verify_weights(st, N, params->spp);  // joins the render into st and checks it
             c->mark_done(st);
-            HIPCHK(hipStreamSynchronize(st));
-            pix[k] = c->h_pixel;
+            npix[k] = N;
         });
     });
     for (int32_t k = 0; k < n_ctx; k++)
@@ -1306,17 +1305,66 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
             if (k) lead->err = "context " + std::to_string(k) + ": " + ctxs[k]->err;
             return -1;
         }
-    const int W = lead->cam.width;
-    for (int32_t k = 0; k < n_ctx; k++)  // Film::merge_tile (core/film.h:85-95), in context order
-        for (size_t i = 0; i < film[k].size(); i++) {
-            const uint32_t px = pix[k][i];
-            const uint64_t p = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
-            radiance[3 * p + 0] += film[k][i].x;
-            radiance[3 * p + 1] += film[k][i].y;
-            radiance[3 * p + 2] += film[k][i].z;
-            weight[p] += film[k][i].w;
+    // Gather on the lead device (Film::merge_tile, core/film.h:85-95): each context's packed film
+    // and pixel list are copied device to device (over xGMI between GPUs), and k_merge_film adds them
+    // into the frame in context order; the frame goes to the host once.
+    return guard(lead, [&] {
+        const int W = lead->cam.width, H = lead->cam.height;
+        const uint64_t F = (uint64_t)W * (uint64_t)H;
+        hipStream_t st = lead->stream;
+        for (int32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->device != lead->device) {
+                const hipError_t e = hipDeviceEnablePeerAccess(ctxs[k]->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+                (void)hipGetLastError();
+            }
+        lead->d_frame.reserve(4 * F);
+        float *frad = lead->d_frame.p, *fw = lead->d_frame.p + 3 * F;
+        HIPCHK(hipMemcpyAsync(frad, radiance, 3 * F * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(fw, weight, F * sizeof(float), hipMemcpyHostToDevice, st));
+        std::vector<uint16_t> seen;
+        for (int32_t k = 0; k < n_ctx; k++) {
+            akr_hip_ctx *c = ctxs[k];
+            const uint64_t N = npix[k];
+            if (N == 0) continue;
+            const float4 *film = c->d_film.p;
+            const uint32_t *pix = c->d_pixel.p;
+            if (c != lead) {
+                HIPCHK(hipStreamWaitEvent(st, c->ev_done, 0));
+                lead->d_gfilm.reserve(N);
+                lead->d_gpix.reserve(N);
+                HIPCHK(hipMemcpyPeerAsync(lead->d_gfilm.p, lead->device, c->d_film.p, c->device, N * sizeof(float4), st));
+                HIPCHK(hipMemcpyPeerAsync(lead->d_gpix.p, lead->device, c->d_pixel.p, c->device, N * sizeof(uint32_t), st));
+                film = lead->d_gfilm.p;
+                pix = lead->d_gpix.p;
+            }
+            // a pixel listed twice (overlapping tiles) goes to successive launches, in list order
+            seen.assign(F, 0);
+            std::vector<std::vector<uint32_t>> rank;
+            for (uint64_t i = 0; i < N; i++) {
+                const uint32_t px = c->h_pixel[i];
+                const uint64_t p = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
+                const uint16_t r = seen[p]++;
+                if (r >= rank.size()) rank.emplace_back();
+                rank[r].push_back((uint32_t)i);
+            }
+            if (rank.size() == 1) {
+                launch_merge_film(film, pix, nullptr, (uint32_t)N, W, frad, fw, st);
+            } else {
+                for (auto &ord : rank) {
+                    lead->d_gorder.upload(ord.data(), ord.size(), st);
+                    launch_merge_film(film, pix, lead->d_gorder.p, (uint32_t)ord.size(), W, frad, fw, st);
+                    HIPCHK(hipStreamSynchronize(st));  // d_gorder is reused by the next launch
+                }
+            }
+            HIPCHK(hipGetLastError());
+            if (c != lead) HIPCHK(hipStreamSynchronize(st));  // the staging buffers are reused
         }
-    return 0;
+        HIPCHK(hipMemcpyAsync(radiance, frad, 3 * F * sizeof(float), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(weight, fw, F * sizeof(float), hipMemcpyDeviceToHost, st));
+        lead->mark_done(st);
+        HIPCHK(hipStreamSynchronize(st));
+    });
 }
 
 namespace {

@@ -21,6 +21,8 @@ void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t s
 void launch_path(bool count, const PathArgs &a, uint32_t grid, hipStream_t st);
 int path_blocks_per_cu();
 void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad, hipStream_t st);
+void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t *order, uint32_t n, int32_t width,
+                       float *rad, float *w, hipStream_t st);
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st);
 
 }  // namespace akr

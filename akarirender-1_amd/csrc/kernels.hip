@@ -1712,6 +1712,24 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     }
 }
 
+// Film::merge_tile (core/film.h:85-95) on the device: a context's packed film (one float4 per
+// slot: radiance sums, weight) added into full-frame buffers at its pixels.  `order` (optional)
+// lists the slots of one launch; a launch never holds the same pixel twice, so the adds of a pixel
+// happen in launch order — the host loop's order.
+__global__ __launch_bounds__(kBlock) void k_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t *order,
+                                                      uint32_t n, int32_t width, float *rad, float *w) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = order ? order[i] : i;
+    const uint32_t px = pixel[j];
+    const size_t p = (size_t)(px & 0xFFFFu) + (size_t)(px >> 16) * (size_t)width;
+    const float4 f = film[j];
+    rad[3 * p + 0] += f.x;
+    rad[3 * p + 1] += f.y;
+    rad[3 * p + 2] += f.z;
+    w[p] += f.w;
+}
+
 __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint32_t n, float *rad, float *w) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -1830,6 +1848,11 @@ int path_blocks_per_cu() {
 void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_check_weights, dim3(blocks_for(n)), dim3(kBlock), 0, st, film, n, expect, bad);
+}
+void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t *order, uint32_t n, int32_t width,
+                       float *rad, float *w, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_merge_film, dim3(blocks_for(n)), dim3(kBlock), 0, st, film, pixel, order, n, width, rad, w);
 }
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
     if (n == 0) return;

@@ -222,8 +222,9 @@ int akr_hip_render_ao(akr_hip_ctx *ctx, const akr_ao_params *params, const akr_r
                       int32_t n_tiles, float *radiance, float *weight);
 /* Multi-GPU render from one host process (SURVEY.md §8b akr_hip_render_node): tile j goes to
  * ctxs[j % n_ctx] (one context per device, each holding the same scene and camera), the contexts
- * render concurrently on one host thread each, and their films are merged into the host buffers
- * in context order — the same pixels as akr_hip_render on one context, bit for bit.
+ * render concurrently on one host thread each, and their films are gathered on ctxs[0]'s device
+ * (device-to-device / xGMI peer copies) and merged there into the frame in context order, which is
+ * added to the host buffers — the same pixels as akr_hip_render on one context, bit for bit.
  * (Multi-process runs over RCCL use akr_hip_render_device + akari_amd/dist.py instead.)
  * On failure the message is on ctxs[0]. */
 int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_params *params,
