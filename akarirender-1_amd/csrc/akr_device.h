@@ -277,6 +277,9 @@ struct PathArgs {
     float ray_clamp;
     uint32_t min_wait;             // a wave processes its waiting lanes once this many wait (or half its live lanes)
     PathProfile *prof;             // counting build only
+    float4 *contrib;               // k_path_defer: per lane, [18][lanes]: 16 NEE contributions awaiting their
+                                   // shadow result (parity * 8 + bounce), then the waiting extension ray
+    uint32_t mix;                  // k_path_defer: scrambled pixel order within each XCD shard
 };
 
 }  // namespace akr

@@ -234,6 +234,14 @@ struct akr_hip_ctx {
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     uint32_t path_grid = 0;   // resident workgroups of the persistent path kernel
+    uint32_t path_grid_defer = 0;  // ... of its deferred-NEE form
+    // option "path_defer": 1 = k_path_defer (max_depth <= 8), 0 = k_path, 2 (default) = k_path_defer for
+    // renders of at most path_defer_pixels pixels (measured on C3, DESIGN.md §3.9: 7 % faster on an
+    // 8-way share, slower on 4-way and larger shares, whose lanes seldom have spare capacity)
+    int path_defer = 2;
+    int64_t path_defer_pixels = 400000;
+    bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
+    DBuf<float4> d_contrib;   // k_path_defer: per-lane NEE contributions awaiting their shadow result
     // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the
     // render has at most path_auto_pixels pixels (measured on C3, DESIGN.md §3.8: the wavefront is ~6 %
     // faster on a whole 1080p frame, k_path 10-33 % faster on a 2-, 4- or 8-way share)
@@ -486,8 +494,9 @@ struct akr_hip_ctx {
             trace_grid[m] = (uint32_t)(n_cu * trace_blocks_per_cu(m));
             mx = std::max(mx, trace_grid[m]);
         }
-        path_grid = (uint32_t)(n_cu * path_blocks_per_cu());
-        mx = std::max(mx, path_grid);
+        path_grid = (uint32_t)(n_cu * path_blocks_per_cu(false));
+        path_grid_defer = (uint32_t)(n_cu * path_blocks_per_cu(true));
+        mx = std::max(mx, std::max(path_grid, path_grid_defer));
         ovf_threads = mx * kTraceBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_ovf_side.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
@@ -788,8 +797,16 @@ struct akr_hip_ctx {
                 pa.ray_clamp = p.ray_clamp;
                 pa.min_wait = (uint32_t)path_min_wait;
                 pa.prof = count ? d_pprof.p : nullptr;
-                const uint32_t grid = (uint32_t)std::min<uint64_t>(path_grid, (N + kTraceBlock - 1) / kTraceBlock);
-                timed("path", ms, [&] { launch_path(count, pa, grid, ms); });
+                const bool defer = p.max_depth <= 8 &&
+                                   (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
+                const uint32_t grid = (uint32_t)std::min<uint64_t>(defer ? path_grid_defer : path_grid,
+                                                                   (N + kTraceBlock - 1) / kTraceBlock);
+                if (defer) {
+                    d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
+                    pa.contrib = d_contrib.p;
+                    pa.mix = path_mix ? 1u : 0u;
+                }
+                timed("path", ms, [&] { launch_path(count, defer, pa, grid, ms); });
                 HIPCHK(hipGetLastError());
             }
             last_passes = 1;
@@ -1060,6 +1077,14 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_auto_pixels = value;
         } else if (k == "any_far_first") {
             ctx->any_far_first = value != 0;
+        } else if (k == "path_defer") {
+            if (value < 0 || value > 2) throw std::runtime_error("path_defer must be 0, 1 or 2 (auto)");
+            ctx->path_defer = (int)value;
+        } else if (k == "path_defer_pixels") {
+            if (value < 0) throw std::runtime_error("path_defer_pixels must be >= 0");
+            ctx->path_defer_pixels = value;
+        } else if (k == "path_mix") {
+            ctx->path_mix = value != 0;
         } else if (k == "path_min_wait") {
             if (value < 1 || value > 64) throw std::runtime_error("path_min_wait must be in [1, 64]");
             ctx->path_min_wait = (int)value;

@@ -1348,6 +1348,182 @@ __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
 #define AKR_PATH_WAVES 4
 #endif
 
+// One lane's ray in the persistent path kernels' traversal loop (k_trace's registers) and the
+// counting build's tallies ([0] closest-hit rays, [1] shadow rays).
+struct PathRay {
+    V3 o, d, invd;
+    float tmin, tmax, tmaxp, best, bu, bv;
+    uint32_t dpos, bgid, cur, leaf;
+    int sp;
+};
+struct PathCount {
+    unsigned long long rays[2] = {0, 0}, box[2] = {0, 0}, tri[2] = {0, 0}, visit[2] = {0, 0}, deep[2] = {0, 0};
+    unsigned long long strav = 0, sleaf = 0, stri = 0, iters = 0;
+    bool deep_now = false;
+};
+
+// B. k_trace's traversal phase over every busy lane's ray (all rays here are lean)
+template <bool COUNT>
+__device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, const float4 *wn, lds_u64 *s_stack,
+                                              glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
+                                              PathCount &c) {
+    while (true) {
+        if (COUNT) {
+            c.strav++;
+            c.sleaf += busy ? 1 : 0;
+            c.iters++;
+        }
+        if (busy && is_internal(r.cur)) {
+            const int nt = visit_wide_lean<false>(wn, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf,
+                                                  ovf_threads, tid, gtid, r.sp);
+            if (COUNT) {
+                c.box[kind] += nt;
+                c.visit[kind]++;
+                c.deep_now = c.deep_now || r.sp > kStackLds;
+            }
+        }
+        if (busy && r.leaf == AKR_CHILD_EMPTY && is_leaf(r.cur)) {
+            r.leaf = r.cur;  // postpone the leaf and keep descending
+            r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
+        }
+        const unsigned long long searching = __ballot(busy && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
+        if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+            (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0))
+            break;
+    }
+}
+
+// C. the leaf phase: the pending leaf's exact box with the current best, then its triangles;
+// returns true when an occlusion ray (kind 1) found its first hit
+template <bool COUNT>
+__device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const float4 *wide_leaves, PathCount &c) {
+    bool hit_any = false;
+    if (busy && r.leaf != AKR_CHILD_EMPTY) {
+        const float4 *lr = wide_leaves + (r.leaf & 0x7FFFFFFFu);
+        const float4 l0 = lr[0], l1 = lr[1];
+        const float4 pa0 = lr[2], pb0 = lr[3], pc0 = lr[4];
+        const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, r.o, r.invd, r.tmin, r.tmax);
+        const bool in = !(tl < 0.0f || tl > r.best);
+        if (COUNT) c.box[kind]++;
+        const uint32_t cnt = in ? fbits(l1.w) : 0u;
+        const float4 *tp = lr + 2;
+        for (uint32_t k = 0; k < cnt; k++) {
+            if (COUNT && lane_prefix(__ballot(1)) == 0) c.stri += 64;
+            const float4 ta = k == 0 ? pa0 : tp[3 * k + 0];
+            const float4 tb = k == 0 ? pb0 : tp[3 * k + 1];
+            const float4 tc = k == 0 ? pc0 : tp[3 * k + 2];
+            if (COUNT) c.tri[kind]++;
+            float t, u, v;
+            if (mt(r.o, r.d, r.tmin, r.tmax, ta, tb, tc, r.best, t, u, v)) {
+                r.best = t;
+                r.bu = u;
+                r.bv = v;
+                r.bgid = fbits(ta.w);
+                if (kind) {
+                    hit_any = true;
+                    break;
+                }
+            }
+        }
+        r.leaf = AKR_CHILD_EMPTY;
+    }
+    return hit_any;
+}
+
+// A fresh ray into the traversal state: lean rays enter the loop (busy), others are traced inline
+// with the exact BVH2 walk and come back finished.  An occlusion ray's best starts at tmax (§3.8).
+template <bool COUNT>
+__device__ __forceinline__ void path_begin(const TraceArgs &a, bool occl, float4 ra, float4 rb, PathRay &r, bool &busy,
+                                           bool &fin, lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid,
+                                           PathCount &c) {
+    r.o = V3{ra.x, ra.y, ra.z};
+    r.d = V3{rb.x, rb.y, rb.z};
+    r.tmin = ra.w;
+    r.tmax = rb.w;
+    r.invd = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    r.dpos = (r.d.x > 0.0f ? 1u : 0u) | (r.d.y > 0.0f ? 2u : 0u) | (r.d.z > 0.0f ? 4u : 0u);
+    if (occl && a.any_far_first) r.dpos ^= 7u;
+    r.tmaxp = float_below(r.tmax);
+    if (COUNT) c.rays[occl]++;
+    if (!lean_ok(r.o, r.invd, r.tmin, r.tmax)) {  // rare: exact BVH2 walk inline (k_trace's exact lane)
+        bool hit;
+        if (occl)
+            trace_exact_core<true, true>(a, r.o, r.d, r.invd, r.tmin, r.tmax, s_stack, ovf, tid, gtid, r.best, r.bu,
+                                         r.bv, r.bgid, hit);
+        else
+            trace_exact_core<false, true>(a, r.o, r.d, r.invd, r.tmin, r.tmax, s_stack, ovf, tid, gtid, r.best, r.bu,
+                                          r.bv, r.bgid, hit);
+        fin = true;
+        return;
+    }
+    r.best = occl ? r.tmax : kInf;
+    r.bu = r.bv = 0.0f;
+    r.bgid = kNoHit;
+    r.sp = 0;
+    r.leaf = AKR_CHILD_EMPTY;
+    if (COUNT) {
+        c.box[occl]++;
+        c.deep_now = false;
+    }
+    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
+    const float4 r0 = nodesf[0], r2 = nodesf[2];
+    const float tr = box_test<true, true>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, r.o, r.invd, r.tmin, r.tmax);
+    r.cur = (a.wide_root == AKR_CHILD_EMPTY || tr < 0.0f || tr > r.best) ? AKR_CHILD_EMPTY : a.wide_root;
+    busy = true;
+}
+
+__device__ __forceinline__ void path_park(uint32_t (*s_park)[kTraceBlock], uint32_t tid, const PathRay &r);
+__device__ __forceinline__ void path_unpark(uint32_t (*s_park)[kTraceBlock], uint32_t tid, PathRay &r, bool far_first,
+                                            bool occl);
+
+// Wave-level pixel fetch from the XCD shards (k_trace's refill): every lane with `need` set gets
+// the next pixel of its wave's shard, or `done` once every shard is exhausted.  With `mix` the
+// fetch order is scrambled within each shard ((i * (2^31 - 1)) mod len, a bijection): the lanes of a
+// wave then hold pixels from all over their shard instead of one tile's rows.
+struct PixelFetch {
+    uint32_t shard, s_lo, s_hi;
+    int shards_left;
+    bool drained;
+};
+__device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t *work, bool mix, bool &need,
+                                             bool &done, uint32_t &pix) {
+    while (true) {
+        const unsigned long long want = __ballot(need && !done);
+        if (want == 0) break;
+        if (f.drained) {
+            if (need) done = true;
+            break;
+        }
+        const uint32_t nw = (uint32_t)__popcll(want);
+        const int leader = __ffsll((long long)want) - 1;
+        uint32_t base = 0;
+        if ((int)__lane_id() == leader) base = atomicAdd(work + f.shard * kWorkStride, nw);
+        base = __shfl(base, leader);
+        if (need && !done) {
+            const uint32_t my = base + lane_prefix(want);
+            const uint32_t len = f.s_hi - f.s_lo;
+            if (base < len && my < len) {
+                pix = f.s_lo + (mix ? (uint32_t)(((uint64_t)my * 2147483647ull) % len) : my);
+                need = false;
+            }
+        }
+        if (base + nw >= f.s_hi - f.s_lo) {  // this shard is exhausted: move to the next open one
+            while (true) {
+                if (--f.shards_left == 0) {
+                    f.drained = true;
+                    break;
+                }
+                f.shard = (f.shard + 1) % kWorkShards;
+                f.s_lo = shard_begin(n, f.shard);
+                f.s_hi = shard_begin(n, f.shard + 1);
+                const uint32_t taken = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(work + f.shard * kWorkStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (taken < f.s_hi - f.s_lo) break;
+            }
+        }
+    }
+}
+
 // The traversal state of every lane is parked in LDS ([field][thread]) while the wave processes its
 // waiting lanes, so the shading code's registers are not stacked on top of it (128 VGPRs and ~80
 // spilled without this); the waiting lanes read their finished ray's result from the same place.
@@ -1467,6 +1643,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         beta = bo.nb;
                         depth++;
                     }
+#ifdef AKR_PROBE_NOSHADOW  // timing probe only (not exact): shadow rays are not traced
+                    bo.sh = false;
+#endif
                     if (bo.sh) {
                         ra = bo.s0;
                         rb = bo.s1;
@@ -1712,6 +1891,388 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     }
 }
 
+__device__ __forceinline__ void path_park(uint32_t (*s_park)[kTraceBlock], uint32_t tid, const PathRay &r) {
+    const float pv[kParkFields] = {r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.tmin, r.tmax, r.best, r.bu, r.bv, bitsf(r.bgid)};
+#pragma unroll
+    for (int k = 0; k < kParkFields; k++) s_park[k][tid] = fbits(pv[k]);
+    s_park[kParkFields][tid] = r.cur;
+    s_park[kParkFields + 1][tid] = (uint32_t)r.sp;
+}
+__device__ __forceinline__ void path_unpark(uint32_t (*s_park)[kTraceBlock], uint32_t tid, PathRay &r, bool far_first,
+                                            bool occl) {
+    r.o = V3{bitsf(s_park[0][tid]), bitsf(s_park[1][tid]), bitsf(s_park[2][tid])};
+    r.d = V3{bitsf(s_park[3][tid]), bitsf(s_park[4][tid]), bitsf(s_park[5][tid])};
+    r.tmin = bitsf(s_park[6][tid]);
+    r.tmax = bitsf(s_park[7][tid]);
+    r.best = bitsf(s_park[8][tid]);
+    r.bu = bitsf(s_park[9][tid]);
+    r.bv = bitsf(s_park[10][tid]);
+    r.bgid = s_park[11][tid];
+    r.cur = s_park[kParkFields][tid];
+    r.sp = (int)s_park[kParkFields + 1][tid];
+    r.invd = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    r.dpos = (r.d.x > 0.0f ? 1u : 0u) | (r.d.y > 0.0f ? 2u : 0u) | (r.d.z > 0.0f ? 4u : 0u);
+    if (occl && far_first) r.dpos ^= 7u;
+    r.tmaxp = float_below(r.tmax);
+    r.leaf = AKR_CHILD_EMPTY;
+}
+
+// Position of the r-th set bit of m (r < popcount(m)): binary search on popcounts
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, uint32_t r) {
+    int base = 0;
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        const unsigned long long low = m & ((1ull << s) - 1ull);
+        const uint32_t c = (uint32_t)__popcll(low);
+        if (r >= c) {
+            r -= c;
+            m >>= s;
+            base += s;
+        } else {
+            m = low;
+        }
+    }
+    return base;
+}
+
+// ------------------------------------------------------------------- persistent path, deferred NEE
+// k_path_defer: k_path with the shadow rays taken off a pixel's chain.  When a bounce
+// yields a shadow ray, its contribution goes to the lane's scratch (slot parity * 8 + bounce) and the
+// ray is handed, by lane shuffles inside the wave, to a lane with no work of its own (pixel done, or
+// waiting on its own shadow results); that lane traces it and posts (resolved, occluded) into the
+// owner's LDS word.  The owner goes on with its extension ray at once.  A sample whose path has ended
+// closes once all its shadow results are in: L = (emission) + the unoccluded contributions in bounce
+// order, exactly the sequential order of pathtracer.h:84-88, then Tile::add_sample.  At most two
+// samples of a pixel are in flight (the older one waiting to close), so the film sums stay in
+// sample order.  A shadow ray with no free lane in the wave is traced by its owner, as in k_path.
+// Every hand-off and result stays inside one wave: no cross-wave synchronisation.
+constexpr uint32_t kDeferSlots = 8;  // shadow rays per sample (one per bounce below max_depth <= 8)
+enum : uint32_t { RAY_NONE = 0, RAY_OWN = 1, RAY_OWN_SHADOW = 2, RAY_FOREIGN = 3 };
+
+// The per-lane sample bookkeeping of k_path_defer in one word (registers are the limit there)
+struct DeferState {
+    uint32_t w = 0;
+    static constexpr uint32_t KIND = 0, RP = 2, LAST = 3, OPEN = 4, NSH = 6, DEPTH = 14, FTAG = 18, PEND = 30, RUN = 31;
+    __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
+    __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
+        const uint32_t m = ((1u << bits) - 1u) << off;
+        w = (w & ~m) | ((v << off) & m);
+    }
+    __device__ __forceinline__ uint32_t kind() const { return get(KIND, 2); }
+    __device__ __forceinline__ uint32_t rp() const { return get(RP, 1); }
+    __device__ __forceinline__ uint32_t last() const { return get(LAST, 1); }
+    __device__ __forceinline__ uint32_t open() const { return get(OPEN, 2); }
+    __device__ __forceinline__ uint32_t nsh(uint32_t q) const { return get(NSH + 4 * q, 4); }
+    __device__ __forceinline__ int depth() const { return (int)get(DEPTH, 4); }
+    __device__ __forceinline__ uint32_t ftag() const { return get(FTAG, 12); }  // owner lane | slot << 8
+    __device__ __forceinline__ bool pend() const { return get(PEND, 1) != 0; }
+    __device__ __forceinline__ bool running() const { return get(RUN, 1) != 0; }
+};
+
+template <bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_defer(PathArgs pa) {
+    const TraceArgs &a = pa.t;
+    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ uint32_t s_park[kParkFields + 2][kTraceBlock];
+    __shared__ uint32_t s_res[kTraceBlock];  // per owner lane: resolved bit (slot), occluded bit (16 + slot)
+    lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
+    glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gtid = blockIdx.x * kTraceBlock + tid;
+    const size_t lanes = (size_t)gridDim.x * kTraceBlock;
+    float4 *const contrib = pa.contrib + gtid;  // slot s at contrib[s * lanes]; 16, 17: the waiting extension ray
+    const uint32_t n = pa.n_pix;
+    const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;
+    const bool ff = a.any_far_first != 0;
+    PathCount c;
+    PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
+    f.s_lo = shard_begin(n, f.shard);
+    f.s_hi = shard_begin(n, f.shard + 1);
+    s_res[tid] = 0;
+
+    uint32_t pix = 0, left = 0, seed = 0, pxy = 0;
+    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f};
+    float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
+    DeferState s;
+    bool need_pixel = true, done = false, fin = false, busy = false;
+    uint32_t idle_rounds = 0;    // hang guard: consecutive rounds with no ray in flight in the wave
+    PathRay r{};
+    r.best = kInf;
+    r.bgid = kNoHit;
+    r.cur = r.leaf = AKR_CHILD_EMPTY;
+    unsigned long long p_outer = 0, p_procs = 0, p_tp = 0, p_tt = 0, p_tl = 0, p_lanes = 0, p_t0 = 0, p_t = 0, p_tsh = 0;
+    if (COUNT) p_t0 = wall_clock64();
+
+    // a new sample of the lane's pixel, when nothing else is in hand and at most one older sample
+    // is still waiting to close (sample k has parity k & 1)
+    auto try_start = [&](bool free_lane, bool &fresh, float4 &ra, float4 &rb) {
+        if (free_lane && !done && !need_pixel && !s.running() && left > 0 && __popc(s.open()) <= 1) {
+            s.set(DeferState::RP, 1, (pa.spp - left) & 1u);
+            left--;
+            s.set(DeferState::RUN, 1, 1);
+            s.set(DeferState::DEPTH, 4, 0);
+            Lr = V3{0.0f, 0.0f, 0.0f};
+            beta = V3{1.0f, 1.0f, 1.0f};
+            camera_ray(pa.cam, (int)(pxy & 0xFFFFu), (int)(pxy >> 16), seed, ra, rb);
+            fresh = true;
+            s.set(DeferState::KIND, 2, RAY_OWN);
+        }
+    };
+
+    while (true) {
+        if (!__any(!done || busy || fin)) break;
+        const uint32_t nfin = (uint32_t)__popcll(__ballot(fin));
+        const uint32_t nbusy = (uint32_t)__popcll(__ballot(busy));
+        if (COUNT) {
+            p_outer++;
+            p_t = wall_clock64();
+        }
+        if (nfin > 0 ? (nfin >= pa.min_wait || 2 * nfin >= nfin + nbusy) : nbusy == 0) {
+            if (COUNT) {
+                p_procs++;
+                p_lanes += nfin;
+            }
+            path_park(s_park, tid, r);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            asm volatile("" ::: "memory");
+            bool fresh = false, occl = false, want_sh = false, sample_end = false;
+            float4 ra = {}, rb = {}, sh0 = {}, sh1 = {};
+            uint32_t shtag = 0;
+            unsigned long long p_ts = 0;
+            if (COUNT) p_ts = wall_clock64();
+            // 1. the finished ray's result
+            if (fin) {
+                fin = false;
+                const uint32_t hgid = s_park[11][tid];
+                const uint32_t kind = s.kind();
+                if (kind == RAY_FOREIGN || kind == RAY_OWN_SHADOW) {
+                    const uint32_t tag = s.ftag();
+                    const uint32_t owner = kind == RAY_FOREIGN ? (tag & 0xFFu) : tid, slot = tag >> 8;
+                    atomicOr(&s_res[owner], (1u << slot) | (hgid != kNoHit ? (1u << (16 + slot)) : 0u));
+                    s.set(DeferState::KIND, 2, RAY_NONE);
+                    if (kind == RAY_OWN_SHADOW && s.pend()) {  // the extension ray waited behind it
+                        ra = contrib[16 * lanes];
+                        rb = contrib[17 * lanes];
+                        s.set(DeferState::PEND, 1, 0);
+                        fresh = true;
+                        s.set(DeferState::KIND, 2, RAY_OWN);
+                    }
+                } else {  // the running sample's closest hit
+                    s.set(DeferState::KIND, 2, RAY_NONE);
+                    if (hgid == kNoHit) {
+                        sample_end = true;
+                    } else {
+                        const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
+                        const int depth = s.depth();
+                        Bounce bo;
+                        shade_hit_call(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
+                                       pa.max_depth, depth == nb - 1, bo);
+                        if (bo.emit) {
+                            Lr.x += bo.e.x;
+                            Lr.y += bo.e.y;
+                            Lr.z += bo.e.z;
+                        }
+                        if (bo.ext) {
+                            beta = bo.nb;
+                            s.set(DeferState::DEPTH, 4, (uint32_t)depth + 1u);
+                        }
+                        if (bo.sh) {
+                            const uint32_t rp = s.rp(), b = s.nsh(rp), slot = rp * kDeferSlots + b;
+                            s.set(DeferState::NSH + 4 * rp, 4, b + 1u);
+                            contrib[slot * lanes] = make_float4(bo.col.x, bo.col.y, bo.col.z, 0.0f);
+                            want_sh = true;
+                            sh0 = bo.s0;
+                            sh1 = bo.s1;
+                            shtag = tid | (slot << 8);
+                            if (bo.ext) {  // may have to wait behind the shadow ray (step 5)
+                                ra = bo.e0;
+                                rb = bo.e1;
+                            } else {
+                                sample_end = true;
+                            }
+                        } else if (bo.ext) {
+                            ra = bo.e0;
+                            rb = bo.e1;
+                            fresh = true;
+                            s.set(DeferState::KIND, 2, RAY_OWN);
+                        } else {
+                            sample_end = true;
+                        }
+                    }
+                }
+            }
+            if (COUNT) p_tsh += wall_clock64() - p_ts;
+            // 2. a path that ended: close at once when nothing waits, else leave it open
+            if (sample_end) {
+                const uint32_t rp = s.rp();
+                s.set(DeferState::RUN, 1, 0);
+                s.set(DeferState::LAST, 1, rp);
+                if (s.nsh(rp) == 0 && s.open() == 0)
+                    splat_one(film, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
+                else
+                    s.set(DeferState::OPEN, 2, s.open() | (1u << rp));
+            }
+            // 3. close the oldest open samples whose shadow results are all in, in sample order
+            for (int it = 0; it < 2 && s.open(); it++) {
+                const uint32_t om = s.open();
+                const uint32_t q = __popc(om) == 2 ? (s.last() ^ 1u) : (om == 1u ? 0u : 1u);
+                const uint32_t k = s.nsh(q);
+                const uint32_t need = ((1u << k) - 1u) << (kDeferSlots * q);
+                const uint32_t res = s_res[tid];
+                if ((res & need) != need) break;
+                V3 L = (q == s.last() && !s.running()) ? Lr : V3{0.0f, 0.0f, 0.0f};
+                for (uint32_t b = 0; b < k; b++)  // pathtracer.h:84-88, in bounce order
+                    if (!((res >> (16 + kDeferSlots * q + b)) & 1u)) {
+                        const float4 cc = contrib[(q * kDeferSlots + b) * lanes];
+                        L.x += cc.x;
+                        L.y += cc.y;
+                        L.z += cc.z;
+                    }
+                splat_one(film, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
+                s.set(DeferState::OPEN, 2, om & ~(1u << q));
+                s.set(DeferState::NSH + 4 * q, 4, 0);
+                atomicAnd(&s_res[tid], ~((0xFFu << (kDeferSlots * q)) | (0xFFu << (16 + kDeferSlots * q))));
+            }
+            // 4. a finished pixel stores its film and fetches the next; free lanes start samples
+            const bool free_lane = !busy && !fresh && !want_sh && s.kind() == RAY_NONE;
+            if (free_lane && !done && !need_pixel && !s.running() && left == 0 && s.open() == 0) {
+                pa.film[pix] = film;
+                need_pixel = true;
+            }
+            const bool asked = need_pixel && !done;
+            fetch_pixels(f, n, pa.work, pa.mix != 0, need_pixel, done, pix);
+            if (asked && !need_pixel) {
+                pxy = pa.pixel[pix];
+                left = pa.spp;
+                seed = (uint32_t)((int)(pxy & 0xFFFFu) + (int)(pxy >> 16) * pa.cam.width);
+                film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+            try_start(free_lane, fresh, ra, rb);
+            // 5. hand the new shadow rays to the wave's lanes that have nothing in hand, in lane order
+            const unsigned long long pm = __ballot(want_sh);
+            if (pm) {
+                const bool helper = !busy && !fresh && !want_sh && s.kind() == RAY_NONE;
+                const unsigned long long hm = __ballot(helper);
+                const uint32_t np = (uint32_t)__popcll(pm), nh = (uint32_t)__popcll(hm);
+                const uint32_t k = np < nh ? np : nh;
+                const uint32_t hr = lane_prefix(hm), pr = lane_prefix(pm);
+                const bool take = helper && hr < k;
+                const int src = take ? nth_set_bit(pm, hr) : (int)__lane_id();
+                float4 x0, x1;
+                x0.x = __shfl(sh0.x, src);
+                x0.y = __shfl(sh0.y, src);
+                x0.z = __shfl(sh0.z, src);
+                x0.w = __shfl(sh0.w, src);
+                x1.x = __shfl(sh1.x, src);
+                x1.y = __shfl(sh1.y, src);
+                x1.z = __shfl(sh1.z, src);
+                x1.w = __shfl(sh1.w, src);
+                const uint32_t tg = (uint32_t)__shfl((int)shtag, src);
+                if (take) {
+                    ra = x0;
+                    rb = x1;
+                    s.set(DeferState::FTAG, 12, tg);
+                    s.set(DeferState::KIND, 2, RAY_FOREIGN);
+                    occl = true;
+                    fresh = true;
+                }
+                if (want_sh) {
+                    const bool has_ext = s.running();  // the path goes on (its ray is in ra / rb)
+                    if (pr < k) {  // handed over: go on with the extension ray, or start the next sample
+                        if (has_ext) {
+                            fresh = true;
+                            s.set(DeferState::KIND, 2, RAY_OWN);
+                        } else {
+                            try_start(true, fresh, ra, rb);
+                        }
+                    } else {  // no free lane: trace it here, the extension ray waits behind it
+                        if (has_ext) {
+                            contrib[16 * lanes] = ra;
+                            contrib[17 * lanes] = rb;
+                            s.set(DeferState::PEND, 1, 1);
+                        }
+                        ra = sh0;
+                        rb = sh1;
+                        s.set(DeferState::FTAG, 12, shtag);
+                        s.set(DeferState::KIND, 2, RAY_OWN_SHADOW);
+                        occl = true;
+                        fresh = true;
+                    }
+                }
+            }
+            asm volatile("" ::: "memory");
+            // 6. unpark; fresh rays begin
+            const uint32_t kind_now = s.kind();
+            path_unpark(s_park, tid, r, ff, kind_now == RAY_OWN_SHADOW || kind_now == RAY_FOREIGN);
+            if (fresh) path_begin<COUNT>(a, occl, ra, rb, r, busy, fin, s_stack, stack_ovf, tid, gtid, c);
+        }
+        if (COUNT) {
+            const unsigned long long t = wall_clock64();
+            p_tp += t - p_t;
+            p_t = t;
+        }
+        if (!__any(busy)) {
+            // nothing in flight: every result is posted, so the next round makes progress; a wave
+            // that idles for many rounds has lost its state (a bug): stop instead of spinning (the
+            // render's in-band weight check then reports it)
+            if (++idle_rounds > 1024) break;
+            continue;
+        }
+        idle_rounds = 0;
+        const uint32_t kind_now = s.kind();
+        const int kd = (kind_now == RAY_OWN_SHADOW || kind_now == RAY_FOREIGN) ? 1 : 0;
+        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
+        if (COUNT) {
+            const unsigned long long t = wall_clock64();
+            p_tt += t - p_t;
+            p_t = t;
+        }
+        const bool hit_any = path_leaf<COUNT>(busy, kd, r, a.wide_leaves, c);
+        if (busy && (hit_any || r.cur == AKR_CHILD_EMPTY)) {
+            busy = false;
+            fin = true;
+            if (COUNT) c.deep[kd] += c.deep_now ? 1 : 0;
+        }
+        if (COUNT) p_tl += wall_clock64() - p_t;
+    }
+    if (COUNT) {
+        if (__lane_id() == 0 && pa.prof) {
+            const unsigned long long tot = wall_clock64() - p_t0;
+            PathProfile &q = *pa.prof;
+            atomicAdd(&q.waves, 1ull);
+            atomicAdd(&q.outer, p_outer);
+            atomicAdd(&q.procs, p_procs);
+            atomicAdd(&q.trav_iters, c.iters);
+            atomicAdd(&q.t_proc, p_tp);
+            atomicAdd(&q.t_trav, p_tt);
+            atomicAdd(&q.t_leaf, p_tl);
+            atomicAdd(&q.t_total, tot);
+            atomicMax(&q.t_max, tot);
+            atomicAdd(&q.lanes_proc, p_lanes);
+            atomicAdd(&q.t_shade, p_tsh);
+        }
+        const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
+        for (int m = 0; m < 2; m++) {
+            const unsigned long long rr = wave_sum(c.rays[m]), b = wave_sum(c.box[m]), t = wave_sum(c.tri[m]),
+                                     v = wave_sum(c.visit[m]), dp = wave_sum(c.deep[m]);
+            if (__lane_id() == 0) {
+                TraceCounters &tc = a.counters[slot_of[m]];
+                atomicAdd(&tc.rays, rr);
+                atomicAdd(&tc.box, b);
+                atomicAdd(&tc.tri, t);
+                atomicAdd(&tc.visits, v);
+                atomicAdd(&tc.deep, dp);
+            }
+        }
+        const unsigned long long st = wave_sum(c.strav), sl = wave_sum(c.sleaf), sr = wave_sum(c.stri);
+        if (__lane_id() == 0) {
+            atomicAdd(&a.counters[TRACE_CLOSEST].slots_trav, st);
+            atomicAdd(&a.counters[TRACE_CLOSEST].slots_leaf, sl);
+            atomicAdd(&a.counters[TRACE_CLOSEST].slots_tri, sr);
+        }
+    }
+}
+
 // Film::merge_tile (core/film.h:85-95) on the device: a context's packed film (one float4 per
 // slot: radiance sums, weight) added into full-frame buffers at its pixels.  `order` (optional)
 // lists the slots of one launch; a launch never holds the same pixel twice, so the adds of a pixel
@@ -1835,14 +2396,21 @@ void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_splat, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
-void launch_path(bool count, const PathArgs &a, uint32_t grid, hipStream_t st) {
+void launch_path(bool count, bool defer, const PathArgs &a, uint32_t grid, hipStream_t st) {
     if (grid == 0) return;
-    if (count) hipLaunchKernelGGL(k_path<true>, dim3(grid), dim3(kTraceBlock), 0, st, a);
-    else hipLaunchKernelGGL(k_path<false>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+    if (defer) {
+        if (count) hipLaunchKernelGGL(k_path_defer<true>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+        else hipLaunchKernelGGL(k_path_defer<false>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+    } else {
+        if (count) hipLaunchKernelGGL(k_path<true>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+        else hipLaunchKernelGGL(k_path<false>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+    }
 }
-int path_blocks_per_cu() {
+int path_blocks_per_cu(bool defer) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false>, kTraceBlock, 0) != hipSuccess || nb <= 0) nb = 1;
+    const hipError_t e = defer ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_defer<false>, kTraceBlock, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false>, kTraceBlock, 0);
+    if (e != hipSuccess || nb <= 0) nb = 1;
     return nb;
 }
 void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad, hipStream_t st) {

@@ -452,26 +452,33 @@ def test_kernel_stats_modes(hip_ctx_factory):
         ctx.set_option("stats", 0)
 
 
-@pytest.mark.parametrize("path", [0, 1])
-def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path):
-    """The persistent path kernel (k_path) and the wavefront kernels give the
-    oracle's image bit for bit: ragged / clipped / empty tiles, depths 0-5, the clamp, Glossy + Mix
-    + two-sided emitter, image textures, a soup whose rays take the deep stack, and a tile list
-    smaller than one workgroup (fewer pixels than lanes)."""
-    with hip_ctx_factory(0) as ctx:
+@pytest.mark.parametrize("path,defer,mix", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)])
+def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix):
+    """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
+    §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
+    scrambled or tile-order pixel fetch) and the wavefront kernels give the oracle's image bit for
+    bit: ragged / clipped / empty tiles, depths 0-9 (above 8 the deferred form falls back to
+    k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
+    deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes)."""
+    def opts(ctx):
         ctx.set_option("path", path)
+        ctx.set_option("path_defer", defer)
+        ctx.set_option("path_mix", mix)
+    with hip_ctx_factory(0) as ctx:
+        opts(ctx)
         cs, orc = _setup(ctx, cornell((40, 24)))
         tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]
-        for spp, depth in ((3, 0), (2, 1), (3, 2), (5, 5)):
+        for spp, depth in ((3, 0), (2, 1), (3, 2), (5, 5), (3, 8), (2, 9)):
             _check_render(ctx, orc, spp, depth, tiles, 40, 24)
         _check_render(ctx, orc, 4, 5, tiles, 40, 24, clamp=10.0)
         _check_render(ctx, orc, 7, 5, [(3, 3, 10, 8)], 40, 24)
     for sc in (mixed_scene((48, 48)), textured_scene((40, 40)), small_soup(100_000, (64, 36))):
         with hip_ctx_factory(0) as ctx:   # one scene per context (uploads append meshes)
-            ctx.set_option("path", path)
+            opts(ctx)
             cs, orc = _setup(ctx, sc)
             W, H = cs.camera.resolution
             _check_render(ctx, orc, 5, 5, [(0, 0, W, H)], W, H)
+            _check_render(ctx, orc, 9, 3, [(0, 0, W, H)], W, H)
 
 
 @pytest.mark.parametrize("spp", [16, 32])
