@@ -247,6 +247,7 @@ struct akr_hip_ctx {
     // faster on a whole 1080p frame, k_path 10-33 % faster on a 2-, 4- or 8-way share)
     int path_kernel = 2;
     int64_t path_auto_pixels = 1500000;
+    bool serial_shadow = false;  // option "serial_shadow": wavefront shadow traces on the main stream (isolated timing)
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
     int path_min_wait = 32;   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
     DBuf<float4> d_trace_rays;
@@ -880,9 +881,16 @@ struct akr_hip_ctx {
                     ts.count = scount(b);
                     ts.shadow_color = d_scolor[sq].p;
                     ts.L = L;
-                    timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, S, side); });
+                    // option serial_shadow (measurement): on the main stream, so the launch is timed alone
+                    hipStream_t sst = serial_shadow ? ms : side;
+                    timed("trace_shadow", sst, [&] { trace_launch(TRACE_SHADOW, tight, ts, S, sst); });
                 }
-                HIPCHK(hipEventRecord(ev_shadow[sq], side));
+                if (serial_shadow) {
+                    HIPCHK(hipEventRecord(ev_shadow[sq], ms));
+                    HIPCHK(hipStreamWaitEvent(side, ev_shadow[sq], 0));
+                } else {
+                    HIPCHK(hipEventRecord(ev_shadow[sq], side));
+                }
             }
             SplatArgs sp{};
             if (la) {
@@ -1075,6 +1083,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_auto_pixels") {
             if (value < 0) throw std::runtime_error("path_auto_pixels must be >= 0");
             ctx->path_auto_pixels = value;
+        } else if (k == "serial_shadow") {
+            ctx->serial_shadow = value != 0;
         } else if (k == "any_far_first") {
             ctx->any_far_first = value != 0;
         } else if (k == "path_defer") {

@@ -315,6 +315,16 @@ def main():
     ctx.render_device(min(K, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
     torch.cuda.synchronize(dev)
     bstats = ctx.kernel_stats()
+    # wavefront form: the shadow trace timed alone (on the main stream, not overlapping the
+    # closest-hit trace of the next bounce), for its own roofline
+    iso = None
+    if "trace_shadow" in bstats:
+        ctx.reset_stats()
+        ctx.set_option("serial_shadow", 1)
+        ctx.render_device(min(K, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        iso = ctx.kernel_stats()
+        ctx.set_option("serial_shadow", 0)
 
     if rank != 0:
         if world > 1:
@@ -373,6 +383,14 @@ def main():
                                    "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
                                for m, c in (("closest", cl), ("shadow", sh))})}
 
+    if iso and "trace_shadow" in iso:   # the shadow trace alone: its own roofline (wavefront form)
+        ks = iso["trace_shadow"]
+        sms = ks["total_ms"] / ks["launches"]
+        sb = ray_bytes(sh) / (cstats.get("trace_shadow", {}).get("launches", 0) or 1)
+        roofline["shadow_isolated"] = {"kernel": "trace_shadow", "avg_launch_ms": sms, "bytes_per_launch": sb,
+                                       "achieved": round(sb / (sms * 1e-3) / 1e9, 1),
+                                       "frac": round(sb / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       "closest_isolated_ms": iso["trace_closest"]["total_ms"] / iso["trace_closest"]["launches"]}
     cpu = None
     if args.cpu_baseline and world == 1:
         sys.path.insert(0, str(ROOT / "oracle"))

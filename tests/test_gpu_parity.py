@@ -441,6 +441,12 @@ def test_kernel_stats_modes(hip_ctx_factory):
             assert np.array_equal(rad, ref)
             ks = ctx.kernel_stats()
             assert set(ks) == expect and ks[key]["launches"] == launches
+        # shadow traces serialised on the main stream (the bench's isolated timing): same image
+        ctx.set_option("path", 0)
+        ctx.set_option("serial_shadow", 1)
+        rad, _ = ctx.render(3, 5, [(0, 0, 32, 32)], 32, 32)
+        assert np.array_equal(rad, ref)
+        ctx.set_option("serial_shadow", 0)
         # auto (the default): the path kernel up to path_auto_pixels pixels, the wavefront above
         ctx.set_option("path", 2)
         ctx.set_option("stats", 2)
