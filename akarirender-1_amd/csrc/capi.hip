@@ -249,7 +249,8 @@ struct akr_hip_ctx {
     int64_t path_auto_pixels = 1500000;
     bool serial_shadow = false;  // option "serial_shadow": wavefront shadow traces on the main stream (isolated timing)
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
-    int path_min_wait = 32;   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
+    int path_min_wait = 32;
+    int path_grid_pct = 100;  // option "path_grid_pct": persistent path grid as a percentage of the resident maximum   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
     DBuf<float4> d_trace_rays;
     DBuf<akr_hit> d_trace_hits;
     // akr_hip_render_node on the lead context: the frame and the staging of other contexts' films
@@ -800,8 +801,9 @@ struct akr_hip_ctx {
                 pa.prof = count ? d_pprof.p : nullptr;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
-                const uint32_t grid = (uint32_t)std::min<uint64_t>(defer ? path_grid_defer : path_grid,
-                                                                   (N + kTraceBlock - 1) / kTraceBlock);
+                const uint64_t resident = (uint64_t)(defer ? path_grid_defer : path_grid) * (uint64_t)path_grid_pct / 100;
+                const uint32_t grid = (uint32_t)std::max<uint64_t>(
+                    1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
                 if (defer) {
                     d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
                     pa.contrib = d_contrib.p;
@@ -1095,6 +1097,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_defer_pixels = value;
         } else if (k == "path_mix") {
             ctx->path_mix = value != 0;
+        } else if (k == "path_grid_pct") {
+            if (value < 1 || value > 100) throw std::runtime_error("path_grid_pct must be in [1, 100]");
+            ctx->path_grid_pct = (int)value;
         } else if (k == "path_min_wait") {
             if (value < 1 || value > 64) throw std::runtime_error("path_min_wait must be in [1, 64]");
             ctx->path_min_wait = (int)value;

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--far-first", default="0", help="occlusion rays far slots first (comma list)")
     ap.add_argument("--defer", default="1", help="k_path_defer (comma list)")
     ap.add_argument("--mix", default="1", help="scrambled pixel fetch in k_path_defer (comma list)")
+    ap.add_argument("--grid-pct", default="100", help="persistent path grid, %% of resident (comma list)")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--builder", default="sbvh")
@@ -67,8 +68,9 @@ def main():
             ctx.set_option("any_far_first", ff)
             ctx.set_option("path_defer", dfr)
             ctx.set_option("path_mix", mx)
-            for mw in (int(x) for x in args.min_wait.split(",")):
+            for mw, gp in ((m, g) for m in (int(x) for x in args.min_wait.split(",")) for g in (int(x) for x in args.grid_pct.split(","))):
                 ctx.set_option("path_min_wait", mw)
+                ctx.set_option("path_grid_pct", gp)
                 res = []
                 for tiles in [full] + [shares[n] for n in splits]:
                     n = dist.n_pixels(tiles)
@@ -78,7 +80,7 @@ def main():
                     ctx.render_device(args.steps, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
                     torch.cuda.synchronize(dev)
                     res.append((time.perf_counter() - t) / args.steps * 1e3)
-                print(f"   path={path} far_first={ff} defer={dfr} mix={mx} min_wait={mw}: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
+                print(f"   path={path} far_first={ff} defer={dfr} mix={mx} min_wait={mw} grid={gp}%: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
                       + "".join(f", {n}-way rank {r:.3f} ms/step (projected {res[0] / r:.2f}x, {W * H / r / 1e3:.0f} Msamples/s)"
                                 for n, r in zip(splits, res[1:])), flush=True)
                 if args.profile and path:
