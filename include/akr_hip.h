@@ -30,6 +30,12 @@
  *
  * Semantics are those of the reference CPU path (no radiance clamp unless ray_clamp > 0,
  * max_depth from the parameters, NEE only, LCG sampler seeded x + y*W per pixel).
+ *
+ * Threading and ordering: a context is bound to one device.  Its traces and renders share the
+ * context's work counters, traversal overflow stacks and queues, so every trace / render call on a
+ * context is ordered after the previous one on the device (an event the next call's stream waits
+ * on), whatever streams the caller passes; calls from several host threads on one context must
+ * still be serialised by the caller.  Different contexts are independent.
  */
 #ifndef AKR_HIP_H
 #define AKR_HIP_H
