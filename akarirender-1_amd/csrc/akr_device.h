@@ -275,7 +275,7 @@ struct PathArgs {
     uint32_t n_pix, spp;
     int32_t max_depth;
     float ray_clamp;
-    uint32_t min_wait;             // a wave processes its waiting lanes once this many wait (or half its live lanes)
+    uint32_t min_wait;             // a wave processes its waiting lanes once min_wait / 64 of its live lanes wait
     PathProfile *prof;             // counting build only
     float4 *contrib;               // k_path_defer: per lane, [18][lanes]: 16 NEE contributions awaiting their
                                    // shadow result (parity * 8 + bounce), then the waiting extension ray

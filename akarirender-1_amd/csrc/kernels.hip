@@ -1583,7 +1583,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             p_outer++;
             p_t = wall_clock64();
         }
-        if (nwait > 0 && (nwait >= pa.min_wait || 2 * nwait >= nwait + nbusy)) {
+        // process once min_wait of a full wave's lanes wait, or that fraction of a sparser wave's
+        if (nwait > 0 && 64u * nwait >= pa.min_wait * (nwait + nbusy)) {
             if (COUNT) {
                 p_procs++;
                 p_lanes += nwait;
@@ -2027,7 +2028,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             p_outer++;
             p_t = wall_clock64();
         }
-        if (nfin > 0 ? (nfin >= pa.min_wait || 2 * nfin >= nfin + nbusy) : nbusy == 0) {
+        if (nfin > 0 ? 64u * nfin >= pa.min_wait * (nfin + nbusy) : nbusy == 0) {
             if (COUNT) {
                 p_procs++;
                 p_lanes += nfin;
