@@ -15,6 +15,15 @@
 #include "../../include/akr_hip.h"
 #include "../../include/akr_bvh_format.h"
 
+// Device code sees the scene record's pointers as global memory (address space 1), so loads through
+// them are global_load even inside an out-of-line function, where the compiler cannot infer it
+// (flat loads also count against lgkmcnt and tie LDS waits to outstanding memory loads).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define AKR_GLOBAL __attribute__((address_space(1)))
+#else
+#define AKR_GLOBAL
+#endif
+
 namespace akr {
 
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
@@ -101,14 +110,14 @@ struct TexDev {
 };
 
 struct SceneDev {
-    const ShadeTri *tri;           // per global triangle id
-    const float *texcoords;        // 6 per triangle (read only when has_image_tex)
+    const AKR_GLOBAL ShadeTri *tri;     // per global triangle id
+    const AKR_GLOBAL float *texcoords;  // 6 per triangle (read only when has_image_tex)
     int32_t has_image_tex;
-    const MatDev *mats;
-    const TexDev *texs;
-    const float *images;
-    const LightDev *lights;
-    const float *light_cdf;        // n_lights + 1
+    const AKR_GLOBAL MatDev *mats;
+    const AKR_GLOBAL TexDev *texs;
+    const AKR_GLOBAL float *images;
+    const AKR_GLOBAL LightDev *lights;
+    const AKR_GLOBAL float *light_cdf;  // n_lights + 1
     int32_t n_lights;
 };
 

@@ -243,10 +243,11 @@ struct akr_hip_ctx {
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     DBuf<float4> d_contrib;   // k_path_defer: per-lane NEE contributions awaiting their shadow result
     // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the
-    // render has at most path_auto_pixels pixels (measured on C3, DESIGN.md §3.8: the wavefront is ~6 %
-    // faster on a whole 1080p frame, k_path 10-33 % faster on a 2-, 4- or 8-way share)
+    // render has at most path_auto_pixels pixels (default: any size; measured on C3, DESIGN.md §3.8,
+    // k_path is 5 % faster than the wavefront on a whole 1080p frame and 19-31 % faster on 2-, 4- and
+    // 8-way shares)
     int path_kernel = 2;
-    int64_t path_auto_pixels = 1500000;
+    int64_t path_auto_pixels = INT64_MAX;
     bool serial_shadow = false;  // option "serial_shadow": wavefront shadow traces on the main stream (isolated timing)
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
     int path_min_wait = 32;
@@ -343,14 +344,14 @@ struct akr_hip_ctx {
 
     SceneDev scene_dev() const {
         SceneDev s{};
-        s.tri = d_shade_tri.p;
-        s.texcoords = d_tc.p;
+        s.tri = (decltype(s.tri))d_shade_tri.p;  // device code sees them as global pointers
+        s.texcoords = (decltype(s.texcoords))d_tc.p;
         s.has_image_tex = has_image_tex ? 1 : 0;
-        s.mats = d_mats.p;
-        s.texs = d_texs.p;
-        s.images = d_images.p;
-        s.lights = d_lights.p;
-        s.light_cdf = d_cdf.p;
+        s.mats = (decltype(s.mats))d_mats.p;
+        s.texs = (decltype(s.texs))d_texs.p;
+        s.images = (decltype(s.images))d_images.p;
+        s.lights = (decltype(s.lights))d_lights.p;
+        s.light_cdf = (decltype(s.light_cdf))d_cdf.p;
         s.n_lights = n_lights;
         return s;
     }

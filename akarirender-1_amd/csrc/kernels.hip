@@ -139,6 +139,7 @@ __device__ __forceinline__ bool is_leaf(uint32_t c) { return (c & AKR_CHILD_LEAF
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 typedef __attribute__((address_space(1))) unsigned long long glb_u64;
 
+
 // Pop the next stacked node whose stored entry distance is not beyond `lim` (the reference
 // re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
 __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_u64 *ovf, uint32_t ovf_threads,
@@ -1036,7 +1037,7 @@ __device__ __forceinline__ V3 tex_eval(const SceneDev &s, int32_t ti, V2 tc) {
     int ix = (int)(x * (float)w), iy = (int)(y * (float)h);
     ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
     iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
-    const float *p = s.images + t.off + 4 * ((int64_t)ix + (int64_t)iy * w);
+    const AKR_GLOBAL float *p = s.images + t.off + 4 * ((int64_t)ix + (int64_t)iy * w);
     return v3(p[0], p[1], p[2]);
 }
 
@@ -1077,10 +1078,10 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     const V3 ns = lerp3(v3(tr.b.w, tr.c.w, tr.d.x), v3(tr.d.y, tr.d.z, tr.d.w), v3(tr.e.x, tr.e.y, tr.e.z), u, v);
     V2 tc{0.0f, 0.0f};  // only image textures read it
     if (s.has_image_tex) {
-        const float *tt = s.texcoords + 6 * (size_t)gid;
+        const AKR_GLOBAL float *tt = s.texcoords + 6 * (size_t)gid;
         tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
     }
-    const MatDev *mat = &s.mats[mid];
+    const AKR_GLOBAL MatDev *mat = &s.mats[mid];
     if (mat->type == AKR_MAT_EMISSIVE) {
         if (depth == 0) {
             const bool face_front = dot(neg(wo), ng) < 0.0f;
@@ -1140,7 +1141,7 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
         }
         int li = hi - 1;
         li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
-        const LightDev &lt = s.lights[li];
+        const AKR_GLOBAL LightDev &lt = s.lights[li];
         const V2 lu = lcg_next2(seed);
         // AreaLight::sample (light.h:58-71); lng, the area and the selection pdf are precomputed
         const float su0 = sqrtf(lu.x);
@@ -1182,7 +1183,7 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
 
 // Out-of-line copy for the persistent path kernel: a call keeps the shading code's registers out of
 // the traversal loop's allocation (the caller saves its few live values around the call).
-__device__ __noinline__ void shade_hit_call(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
+__device__ __noinline__ void shade_hit_call(const SceneDev s, uint32_t gid, float u, float v, V3 wo, V3 beta,
                                             uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
     shade_hit(s, gid, u, v, wo, beta, seed, depth, max_depth, last, o);
 }
