@@ -66,7 +66,15 @@ def main(tag):
         if p.exists():
             lines = [l for l in p.read_text().splitlines() if l.startswith("{")]
             if lines:
-                workload = json.loads(lines[-1])["config"]
+                line = json.loads(lines[-1])
+                workload = line["config"]
+                # a persistent path launch renders every spp of its call: bytes per sample pass
+                # (bench.py launches warmup W, timed K and an untimed breakdown of min(K, 4) spp)
+                K, Wm = line["steps"], line["warmup"]
+                spp_total = (Wm if Wm > 0 else 0) + K + min(K, 4)
+                for k, t in traffic.items():
+                    if k.startswith("k_path") and "true" not in k and t["launches_sampled"]:
+                        t["hbm_bytes_per_spp"] = t["hbm_bytes_per_launch"] * t["launches_sampled"] / spp_total
     (dst / f"{tag}_traffic.json").write_text(json.dumps(
         {"tag": tag, "workload": workload, "source": f"profiles/{tag}_pmc_fetch.csv + {tag}_pmc_write.csv",
          "kernels": traffic}, indent=1) + "\n")
