@@ -1181,8 +1181,10 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     }
 }
 
-// Out-of-line copy for the persistent path kernel: a call keeps the shading code's registers out of
-// the traversal loop's allocation (the caller saves its few live values around the call).
+// Out-of-line copy for the persistent path kernels (build option AKR_PATH_CALL_SHADE): a call keeps the
+// shading code's registers out of the traversal loop's allocation, at the price of saving the live
+// values around it in scratch.  With flat loads it was the only spill-free form; with global loads
+// the inlined form measured 3 % faster.
 __device__ __noinline__ void shade_hit_call(const SceneDev s, uint32_t gid, float u, float v, V3 wo, V3 beta,
                                             uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
     shade_hit(s, gid, u, v, wo, beta, seed, depth, max_depth, last, o);
@@ -1628,7 +1630,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #ifdef AKR_PROBE_NOSHADE
                     bo.emit = false; bo.sh = false; bo.ext = hgid & 1; bo.e0 = make_float4(wo.x, wo.y, wo.z, 1.f); bo.e1 = bo.e0; bo.nb = wo;
 #else
-#ifdef AKR_PATH_INLINE_SHADE
+#ifndef AKR_PATH_CALL_SHADE  // inlined (default): 3 % faster than the out-of-line call once every load is global
                     shade_hit(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
                               pa.max_depth, depth == nb - 1, bo);
 #else
@@ -2067,8 +2069,13 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
                         const int depth = s.depth();
                         Bounce bo;
+#ifndef AKR_PATH_CALL_SHADE  // inlined (default): 3 % faster than the out-of-line call once every load is global
+                        shade_hit(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
+                                  pa.max_depth, depth == nb - 1, bo);
+#else
                         shade_hit_call(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
                                        pa.max_depth, depth == nb - 1, bo);
+#endif
                         if (bo.emit) {
                             Lr.x += bo.e.x;
                             Lr.y += bo.e.y;
