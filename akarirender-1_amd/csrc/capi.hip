@@ -196,6 +196,7 @@ struct akr_hip_ctx {
     float func_int = 0;
     int32_t n_lights = 0;
     bool has_image_tex = false;
+    bool simple_shading = true;  // every material Diffuse / Emissive with constant textures
 
     CameraDev cam{};
     bool cam_set = false;
@@ -248,6 +249,7 @@ struct akr_hip_ctx {
     // 8-way shares)
     int path_kernel = 2;
     int64_t path_auto_pixels = INT64_MAX;
+    bool path_auto_complex = false;  // option "path_auto_complex": auto also takes k_path for complex shading
     bool serial_shadow = false;  // option "serial_shadow": wavefront shadow traces on the main stream (isolated timing)
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
     int path_min_wait = 32;
@@ -375,12 +377,16 @@ struct akr_hip_ctx {
             else ok = false;
             if (!ok) throw std::runtime_error("material " + std::to_string(m) + " has an invalid type or reference");
         }
+        // shading the persistent path kernels run well inline: constant Diffuse / Emissive only
+        simple_shading = true;
+        for (auto &m : mats) simple_shading = simple_shading && (m.type == AKR_MAT_DIFFUSE || m.type == AKR_MAT_EMISSIVE);
         has_image_tex = false;
         for (auto &t : texs) {
             if (t.type == AKR_TEX_IMAGE && (t.image < 0 || t.image >= (int32_t)img_w.size()))
                 throw std::runtime_error("image texture references a missing image");
             has_image_tex = has_image_tex || t.type == AKR_TEX_IMAGE;
         }
+        simple_shading = simple_shading && !has_image_tex;
         // one 80-byte shading record per triangle: corners, per-face-vertex normals, material
         std::vector<ShadeTri> st(nt);
         for (uint64_t g = 0; g < nt; g++) {
@@ -783,7 +789,11 @@ struct akr_hip_ctx {
         // Persistent path kernel: every sample of every pixel in one launch.  It
         // runs the lean wide traversal only; the reference cull, the BVH2 kernel, a wide view whose
         // frames exceed the lean test's bounds and lookahead lanes keep the wavefront form.
-        const bool use_path = path_kernel == 1 || (path_kernel == 2 && (int64_t)N <= path_auto_pixels);
+        // auto: the persistent kernel for scenes whose shading is constant Diffuse / Emissive; Glossy,
+        // Mix or image textures diverge inside the traversal waves, and the wavefront's separate shade
+        // kernel measured faster there (textured hall 11.5 vs 16.0 ms per 4K spp)
+        const bool use_path = path_kernel == 1 || (path_kernel == 2 && (int64_t)N <= path_auto_pixels &&
+                                                   (simple_shading || path_auto_complex));
         if (use_path && tight && wide && !la && trace_args(nullptr).lean) {
             if (p.spp > 0) {
                 HIPCHK(hipMemsetAsync(d_counts.p, 0, kWorkWords * sizeof(uint32_t), ms));
@@ -1083,6 +1093,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path") {
             if (value < 0 || value > 2) throw std::runtime_error("path must be 0 (wavefront), 1 (path kernel) or 2 (auto)");
             ctx->path_kernel = (int)value;
+        } else if (k == "path_auto_complex") {
+            ctx->path_auto_complex = value != 0;
         } else if (k == "path_auto_pixels") {
             if (value < 0) throw std::runtime_error("path_auto_pixels must be >= 0");
             ctx->path_auto_pixels = value;

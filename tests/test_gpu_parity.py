@@ -458,6 +458,23 @@ def test_kernel_stats_modes(hip_ctx_factory):
         ctx.set_option("stats", 0)
 
 
+def test_auto_form_by_shading(hip_ctx_factory):
+    """Auto dispatch: constant Diffuse / Emissive scenes render with the persistent
+    kernel, scenes with Glossy / Mix materials or image textures with the wavefront (whose shade
+    kernel measured faster there), unless path_auto_complex asks for the persistent kernel; every
+    form gives the oracle's image."""
+    for sc, simple in ((cornell((32, 32)), True), (mixed_scene((32, 32)), False), (textured_scene((32, 32)), False)):
+        with hip_ctx_factory(0) as ctx:
+            cs, orc = _setup(ctx, sc)
+            ctx.set_option("stats", 2)
+            for complex_ok in (0, 1):
+                ctx.set_option("path_auto_complex", complex_ok)
+                ctx.reset_stats()
+                _check_render(ctx, orc, 3, 5, [(0, 0, 32, 32)], 32, 32)
+                want = "path" if (simple or complex_ok) else "trace_closest"
+                assert set(ctx.kernel_stats()) == {want}, (sc, complex_ok, ctx.kernel_stats())
+
+
 @pytest.mark.parametrize("path,defer,mix", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)])
 def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,

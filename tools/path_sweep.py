@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--builder", default="sbvh")
+    ap.add_argument("--scene", choices=["soup", "hall", "cornell"], default="soup")
     ap.add_argument("--profile", type=int, default=0, help="also print the counted k_path phase profile")
     ap.add_argument("--splits", default="8", help="emulated ranks of the tile split to time besides the full frame")
     args = ap.parse_args()
@@ -44,7 +45,7 @@ def main():
     import torch
     from akari_amd import dist
     dev = torch.device("cuda", 0)
-    W, H = 1920, 1080
+    W, H = (3840, 2160) if args.scene == "hall" else (1920, 1080)
     full = dist.tile_grid(W, H, 32)
     splits = [int(x) for x in args.splits.split(",")]
     shares = {n: dist.tiles_for_rank(W, H, 32, 0, n) for n in splits}
@@ -55,7 +56,14 @@ def main():
         os.environ["AKR_HIP_LIB"] = lib
         import akari_amd.capi as capi
         import akari_amd.scene as scene
-        cs = scene.compile_scene(scene.soup_scene(n_tris=args.tris, resolution=(W, H)))  # this module's types
+        if args.scene == "hall":
+            sc = scene.hall_scene(resolution=(W, H))
+        elif args.scene == "cornell":
+            sc = scene.cornell_scene(Path(__file__).resolve().parent.parent / "tests" / "golden" / "CornellBox-Original.obj.mesh",
+                                     resolution=(W, H))
+        else:
+            sc = scene.soup_scene(n_tris=args.tris, resolution=(W, H))
+        cs = scene.compile_scene(sc)  # this module's types
         ctx = capi.HipContext(0)
         t0 = time.time()
         scene.upload_scene(ctx, cs, builder={"sah": capi.BUILDER_SAH, "sbvh": capi.BUILDER_SBVH,
