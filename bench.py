@@ -383,6 +383,9 @@ def main():
                                    "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
                                for m, c in (("closest", cl), ("shadow", sh))})}
 
+    if achieved > HBM_PEAK_GBS:   # small scenes: the BVH lives in L2, so the model bytes are not HBM bytes
+        roofline["note"] = ("algorithmic bytes exceed the HBM peak: the BVH is cache-resident, HBM does not bound "
+                            "this scene (SURVEY.md §8d C2)")
     if iso and "trace_shadow" in iso:   # the shadow trace alone: its own roofline (wavefront form)
         ks = iso["trace_shadow"]
         sms = ks["total_ms"] / ks["launches"]
