@@ -1433,12 +1433,13 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
     return hit_any;
 }
 
-// A fresh ray into the traversal state: lean rays enter the loop (busy), others are traced inline
-// with the exact BVH2 walk and come back finished.  An occlusion ray's best starts at tmax (§3.8).
+// A fresh ray into the traversal state: lean rays enter the loop (returns true: the lane is busy),
+// others are traced inline with the exact BVH2 walk and come back finished (false).  An occlusion
+// ray's best starts at tmax (§3.8).  A return value, not bool references: a reference to one of two
+// flags picked per lane puts both in scratch.
 template <bool COUNT>
-__device__ __forceinline__ void path_begin(const TraceArgs &a, bool occl, float4 ra, float4 rb, PathRay &r, bool &busy,
-                                           bool &fin, lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid,
-                                           PathCount &c) {
+__device__ __forceinline__ bool path_begin(const TraceArgs &a, bool occl, float4 ra, float4 rb, PathRay &r,
+                                           lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid, PathCount &c) {
     r.o = V3{ra.x, ra.y, ra.z};
     r.d = V3{rb.x, rb.y, rb.z};
     r.tmin = ra.w;
@@ -1456,8 +1457,7 @@ __device__ __forceinline__ void path_begin(const TraceArgs &a, bool occl, float4
         else
             trace_exact_core<false, true>(a, r.o, r.d, r.invd, r.tmin, r.tmax, s_stack, ovf, tid, gtid, r.best, r.bu,
                                           r.bv, r.bgid, hit);
-        fin = true;
-        return;
+        return false;
     }
     r.best = occl ? r.tmax : kInf;
     r.bu = r.bv = 0.0f;
@@ -1472,7 +1472,7 @@ __device__ __forceinline__ void path_begin(const TraceArgs &a, bool occl, float4
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const float tr = box_test<true, true>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, r.o, r.invd, r.tmin, r.tmax);
     r.cur = (a.wide_root == AKR_CHILD_EMPTY || tr < 0.0f || tr > r.best) ? AKR_CHILD_EMPTY : a.wide_root;
-    busy = true;
+    return true;
 }
 
 __device__ __forceinline__ void path_park(uint32_t (*s_park)[kTraceBlock], uint32_t tid, const PathRay &r);
@@ -1527,6 +1527,49 @@ __device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t
     }
 }
 
+// Counting build: a wave's phase profile and ray tallies into PathProfile / TraceCounters
+__device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &c, unsigned long long p_outer,
+                                                 unsigned long long p_procs, unsigned long long p_tp,
+                                                 unsigned long long p_tt, unsigned long long p_tl, unsigned long long p_t0,
+                                                 unsigned long long p_lanes, unsigned long long p_tsh) {
+    const TraceArgs &a = pa.t;
+    if (__lane_id() == 0 && pa.prof) {
+        const unsigned long long tot = wall_clock64() - p_t0;
+        PathProfile &q = *pa.prof;
+        atomicAdd(&q.waves, 1ull);
+        atomicAdd(&q.outer, p_outer);
+        atomicAdd(&q.procs, p_procs);
+        atomicAdd(&q.trav_iters, c.iters);
+        atomicAdd(&q.t_proc, p_tp);
+        atomicAdd(&q.t_trav, p_tt);
+        atomicAdd(&q.t_leaf, p_tl);
+        atomicAdd(&q.t_total, tot);
+        atomicMax(&q.t_max, tot);
+        atomicAdd(&q.lanes_proc, p_lanes);
+        atomicAdd(&q.t_shade, p_tsh);
+    }
+    const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
+    for (int m = 0; m < 2; m++) {
+        const unsigned long long rr = wave_sum(c.rays[m]), b = wave_sum(c.box[m]), t = wave_sum(c.tri[m]),
+                                 v = wave_sum(c.visit[m]), dp = wave_sum(c.deep[m]);
+        if (__lane_id() == 0) {
+            TraceCounters &tc = a.counters[slot_of[m]];
+            atomicAdd(&tc.rays, rr);
+            atomicAdd(&tc.box, b);
+            atomicAdd(&tc.tri, t);
+            atomicAdd(&tc.visits, v);
+            atomicAdd(&tc.deep, dp);
+        }
+    }
+    // lane-slot utilisation of the shared loop: under the closest-hit set
+    const unsigned long long st = wave_sum(c.strav), sl = wave_sum(c.sleaf), sr = wave_sum(c.stri);
+    if (__lane_id() == 0) {
+        atomicAdd(&a.counters[TRACE_CLOSEST].slots_trav, st);
+        atomicAdd(&a.counters[TRACE_CLOSEST].slots_leaf, sl);
+        atomicAdd(&a.counters[TRACE_CLOSEST].slots_tri, sr);
+    }
+}
+
 // The traversal state of every lane is parked in LDS ([field][thread]) while the wave processes its
 // waiting lanes, so the shading code's registers are not stacked on top of it (128 VGPRs and ~80
 // spilled without this); the waiting lanes read their finished ray's result from the same place.
@@ -1541,21 +1584,13 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
     const uint32_t gtid = blockIdx.x * kTraceBlock + tid;
-    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
-    const uint32_t root = a.wide_root;
-    const float4 *wn = a.wide_nodes;
     const uint32_t n = pa.n_pix;
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
-    // COUNT: [0] closest-hit rays, [1] shadow rays
-    unsigned long long c_rays[2] = {0, 0}, c_box[2] = {0, 0}, c_tri[2] = {0, 0}, c_visit[2] = {0, 0}, c_deep[2] = {0, 0};
-    unsigned long long c_strav = 0, c_sleaf = 0, c_stri = 0;
-    bool deep = false;
-
-    // pixel fetch: kWorkShards contiguous ranges of the pixel list, one counter each (as k_trace)
-    uint32_t shard = blockIdx.x % kWorkShards;
-    int shards_left = kWorkShards;
-    uint32_t s_lo = shard_begin(n, shard), s_hi = shard_begin(n, shard + 1);
-    bool drained = n == 0;
+    const bool ff = a.any_far_first != 0;
+    PathCount c;
+    PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
+    f.s_lo = shard_begin(n, f.shard);
+    f.s_hi = shard_begin(n, f.shard + 1);
 
     // per-lane path state
     uint32_t pix = 0, left = 0, seed = 0;
@@ -1564,16 +1599,13 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
     float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
     bool pend = false;
-    bool any = false;           // the current ray is a shadow ray
-    bool need_pixel = true, done = false, fin = false;
-    // traversal state (k_trace); a shadow ray's hit is bgid != kNoHit
-    V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
-    float tmin = 0.0f, tmax = 0.0f, tmaxp = 0.0f, best = kInf, bu = 0.0f, bv = 0.0f;
-    uint32_t dpos = 0, bgid = kNoHit, cur = AKR_CHILD_EMPTY, leaf = AKR_CHILD_EMPTY;
-    int sp = 0;
-    bool busy = false;
-    unsigned long long p_outer = 0, p_procs = 0, p_iters = 0, p_tp = 0, p_tt = 0, p_tl = 0, p_lanes = 0, p_t0 = 0, p_t = 0,
-                       p_tsh = 0;
+    bool any = false;           // the lane's ray is a shadow ray (a hit is bgid != kNoHit)
+    bool need_pixel = true, done = false, fin = false, busy = false;
+    PathRay r{};
+    r.best = kInf;
+    r.bgid = kNoHit;
+    r.cur = r.leaf = AKR_CHILD_EMPTY;
+    unsigned long long p_outer = 0, p_procs = 0, p_tp = 0, p_tt = 0, p_tl = 0, p_lanes = 0, p_t0 = 0, p_t = 0, p_tsh = 0;
     if (COUNT) p_t0 = wall_clock64();
 
     while (true) {
@@ -1592,13 +1624,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 p_procs++;
                 p_lanes += nwait;
             }
-            {   // park
-                const float pv[kParkFields] = {o.x, o.y, o.z, d.x, d.y, d.z, tmin, tmax, best, bu, bv, bitsf(bgid)};
-#pragma unroll
-                for (int k = 0; k < kParkFields; k++) s_park[k][tid] = fbits(pv[k]);
-                s_park[kParkFields][tid] = cur;
-                s_park[kParkFields + 1][tid] = (uint32_t)sp;
-            }
+            path_park(s_park, tid, r);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             asm volatile("" ::: "memory");
             bool fresh = false, next_any = false, sample_end = false, start = false;
@@ -1627,16 +1653,14 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 } else {
                     const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
                     Bounce bo;
-#ifdef AKR_PROBE_NOSHADE
+#ifdef AKR_PROBE_NOSHADE  // timing probe only: no shading
                     bo.emit = false; bo.sh = false; bo.ext = hgid & 1; bo.e0 = make_float4(wo.x, wo.y, wo.z, 1.f); bo.e1 = bo.e0; bo.nb = wo;
-#else
-#ifndef AKR_PATH_CALL_SHADE  // inlined (default): 3 % faster than the out-of-line call once every load is global
+#elif !defined(AKR_PATH_CALL_SHADE)  // inlined (default): 3 % faster than the out-of-line call once every load is global
                     shade_hit(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
                               pa.max_depth, depth == nb - 1, bo);
 #else
                     shade_hit_call(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
                                    pa.max_depth, depth == nb - 1, bo);
-#endif
 #endif
                     if (bo.emit) {
                         Lr.x += bo.e.x;
@@ -1650,7 +1674,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #ifdef AKR_PROBE_NOSHADOW  // timing probe only (not exact): shadow rays are not traced
                     bo.sh = false;
 #endif
-                    if (bo.sh) {
+                    if (bo.sh) {  // the shadow ray first, the extension ray waits behind it
                         ra = bo.s0;
                         rb = bo.s1;
                         scol = bo.col;
@@ -1679,106 +1703,29 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 }
             }
             // next pixel for the lanes that finished theirs: one atomic per wave per attempt
-            while (true) {
-                const unsigned long long want = __ballot(need_pixel && !done);
-                if (want == 0) break;
-                if (drained) {
-                    if (need_pixel) done = true;
-                    break;
-                }
-                const uint32_t nw = (uint32_t)__popcll(want);
-                const int leader = __ffsll((long long)want) - 1;
-                uint32_t base = 0;
-                if ((int)__lane_id() == leader) base = atomicAdd(pa.work + shard * kWorkStride, nw);
-                base = __shfl(base, leader);
-                if (need_pixel && !done) {
-                    const uint32_t my = s_lo + base + lane_prefix(want);
-                    if (base < s_hi - s_lo && my < s_hi) {
-                        pix = my;
-                        left = pa.spp;
-                        const uint32_t px = pa.pixel[pix];
-                        seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
-                        film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        need_pixel = false;
-                        start = true;
-                    }
-                }
-                if (base + nw >= s_hi - s_lo) {  // this shard is exhausted: move to the next open one
-                    while (true) {
-                        if (--shards_left == 0) {
-                            drained = true;
-                            break;
-                        }
-                        shard = (shard + 1) % kWorkShards;
-                        s_lo = shard_begin(n, shard);
-                        s_hi = shard_begin(n, shard + 1);
-                        const uint32_t taken = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                            pa.work + shard * kWorkStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                        if (taken < s_hi - s_lo) break;
-                    }
-                }
+            const bool asked = need_pixel && !done;
+            fetch_pixels(f, n, pa.work, false, need_pixel, done, pix);
+            if (asked && !need_pixel) {
+                const uint32_t px = pa.pixel[pix];
+                left = pa.spp;
+                seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                start = true;
             }
             if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
                 Lr = V3{0.0f, 0.0f, 0.0f};
                 beta = V3{1.0f, 1.0f, 1.0f};
                 depth = 0;
-                const uint32_t px = pa.pixel[pix];
+                const uint32_t px = pa.pixel[pix];  // reloaded: cheaper than a register live across the loop
                 camera_ray(pa.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, ra, rb);
                 fresh = true;
             }
             asm volatile("" ::: "memory");
-            {   // unpark (the busy lanes' traversal continues unchanged)
-                o = V3{bitsf(s_park[0][tid]), bitsf(s_park[1][tid]), bitsf(s_park[2][tid])};
-                d = V3{bitsf(s_park[3][tid]), bitsf(s_park[4][tid]), bitsf(s_park[5][tid])};
-                tmin = bitsf(s_park[6][tid]);
-                tmax = bitsf(s_park[7][tid]);
-                best = bitsf(s_park[8][tid]);
-                bu = bitsf(s_park[9][tid]);
-                bv = bitsf(s_park[10][tid]);
-                bgid = s_park[11][tid];
-                cur = s_park[kParkFields][tid];
-                sp = (int)s_park[kParkFields + 1][tid];
-                invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-                dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
-                if (any && a.any_far_first) dpos ^= 7u;
-                tmaxp = float_below(tmax);
-            }
+            path_unpark(s_park, tid, r, ff, any);  // the busy lanes' traversal continues unchanged
             if (fresh) {
                 any = next_any;
-                o = V3{ra.x, ra.y, ra.z};
-                d = V3{rb.x, rb.y, rb.z};
-                tmin = ra.w;
-                tmax = rb.w;
-                invd = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-                dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
-                if (any && a.any_far_first) dpos ^= 7u;
-                tmaxp = float_below(tmax);
-                if (COUNT) c_rays[any]++;
-                if (!lean_ok(o, invd, tmin, tmax)) {
-                    // rare: exact BVH2 walk inline (k_trace's exact lane)
-                    bool occ;
-                    if (any)
-                        trace_exact_core<true, true>(a, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid, best, bu, bv,
-                                                     bgid, occ);
-                    else
-                        trace_exact_core<false, true>(a, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid, best, bu, bv,
-                                                      bgid, occ);
-                    fin = true;
-                } else {
-                    best = any ? tmax : kInf;
-                    bu = bv = 0.0f;
-                    bgid = kNoHit;
-                    sp = 0;
-                    leaf = AKR_CHILD_EMPTY;
-                    if (COUNT) {
-                        c_box[any]++;
-                        deep = false;
-                    }
-                    const float4 r0 = nodesf[0], r2 = nodesf[2];
-                    const float tr = box_test<true, true>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
-                    cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > best) ? AKR_CHILD_EMPTY : root;
-                    busy = true;
-                }
+                busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
+                fin = !busy;
             }
         }
         if (COUNT) {
@@ -1787,112 +1734,23 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             p_t = t;
         }
         if (!__any(busy)) continue;
-        // ---- B. traversal phase (k_trace; every ray here is lean)
-        while (true) {
-            if (COUNT) {
-                c_strav++;
-                c_sleaf += busy ? 1 : 0;
-                p_iters++;
-            }
-            if (busy && is_internal(cur)) {
-                const int nt = visit_wide_lean<false>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
-                                                      a.ovf_threads, tid, gtid, sp);
-                if (COUNT) {
-                    c_box[any] += nt;
-                    c_visit[any]++;
-                    deep = deep || sp > kStackLds;
-                }
-            }
-            if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
-                leaf = cur;  // postpone the leaf and keep descending
-                cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, best);
-            }
-            const unsigned long long searching = __ballot(busy && leaf == AKR_CHILD_EMPTY && cur != AKR_CHILD_EMPTY);
-            if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
-                (searching == 0 || __ballot(busy && leaf != AKR_CHILD_EMPTY) != 0))
-                break;
-        }
+        // ---- B. traversal phase, C. leaf phase (k_trace's, shared with k_path_defer)
+        const int kd = any ? 1 : 0;
+        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
         if (COUNT) {
             const unsigned long long t = wall_clock64();
             p_tt += t - p_t;
             p_t = t;
         }
-        // ---- C. leaf phase: the leaf's exact box with the current best, then its triangles
-        bool hit_any = false;
-        if (busy && leaf != AKR_CHILD_EMPTY) {
-            const float4 *lr = a.wide_leaves + (leaf & 0x7FFFFFFFu);
-            const float4 l0 = lr[0], l1 = lr[1];
-            const float4 pa0 = lr[2], pb0 = lr[3], pc0 = lr[4];
-            const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
-            const bool in = !(tl < 0.0f || tl > best);
-            if (COUNT) c_box[any]++;
-            const uint32_t cnt = in ? fbits(l1.w) : 0u;
-            const float4 *tp = lr + 2;
-            for (uint32_t k = 0; k < cnt; k++) {
-                if (COUNT && lane_prefix(__ballot(1)) == 0) c_stri += 64;
-                const float4 ta = k == 0 ? pa0 : tp[3 * k + 0];
-                const float4 tb = k == 0 ? pb0 : tp[3 * k + 1];
-                const float4 tc = k == 0 ? pc0 : tp[3 * k + 2];
-                if (COUNT) c_tri[any]++;
-                float t, u, v;
-                if (mt(o, d, tmin, tmax, ta, tb, tc, best, t, u, v)) {
-                    best = t;
-                    bu = u;
-                    bv = v;
-                    bgid = fbits(ta.w);
-                    if (any) {
-                        hit_any = true;
-                        break;
-                    }
-                }
-            }
-            leaf = AKR_CHILD_EMPTY;
-        }
-        if (busy && (hit_any || cur == AKR_CHILD_EMPTY)) {
+        const bool hit_any = path_leaf<COUNT>(busy, kd, r, a.wide_leaves, c);
+        if (busy && (hit_any || r.cur == AKR_CHILD_EMPTY)) {
             busy = false;
             fin = true;
-            if (COUNT) c_deep[any] += deep ? 1 : 0;
+            if (COUNT) c.deep[kd] += c.deep_now ? 1 : 0;
         }
         if (COUNT) p_tl += wall_clock64() - p_t;
     }
-    if (COUNT) {
-        if (__lane_id() == 0 && pa.prof) {
-            const unsigned long long tot = wall_clock64() - p_t0;
-            PathProfile &q = *pa.prof;
-            atomicAdd(&q.waves, 1ull);
-            atomicAdd(&q.outer, p_outer);
-            atomicAdd(&q.procs, p_procs);
-            atomicAdd(&q.trav_iters, p_iters);
-            atomicAdd(&q.t_proc, p_tp);
-            atomicAdd(&q.t_trav, p_tt);
-            atomicAdd(&q.t_leaf, p_tl);
-            atomicAdd(&q.t_total, tot);
-            atomicMax(&q.t_max, tot);
-            atomicAdd(&q.lanes_proc, p_lanes);
-            atomicAdd(&q.t_shade, p_tsh);
-        }
-        const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
-        for (int m = 0; m < 2; m++) {
-            const unsigned long long r = wave_sum(c_rays[m]), b = wave_sum(c_box[m]), t = wave_sum(c_tri[m]),
-                                     v = wave_sum(c_visit[m]), dp = wave_sum(c_deep[m]);
-            if (__lane_id() == 0) {
-                TraceCounters &tc = a.counters[slot_of[m]];
-                atomicAdd(&tc.rays, r);
-                atomicAdd(&tc.box, b);
-                atomicAdd(&tc.tri, t);
-                atomicAdd(&tc.visits, v);
-                atomicAdd(&tc.deep, dp);
-            }
-        }
-        c_strav = wave_sum(c_strav);
-        c_sleaf = wave_sum(c_sleaf);
-        c_stri = wave_sum(c_stri);
-        if (__lane_id() == 0) {  // lane-slot utilisation of the shared loop: under the closest-hit set
-            atomicAdd(&a.counters[TRACE_CLOSEST].slots_trav, c_strav);
-            atomicAdd(&a.counters[TRACE_CLOSEST].slots_leaf, c_sleaf);
-            atomicAdd(&a.counters[TRACE_CLOSEST].slots_tri, c_stri);
-        }
-    }
+    if (COUNT) path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
 }
 
 __device__ __forceinline__ void path_park(uint32_t (*s_park)[kTraceBlock], uint32_t tid, const PathRay &r) {
@@ -2213,7 +2071,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             // 6. unpark; fresh rays begin
             const uint32_t kind_now = s.kind();
             path_unpark(s_park, tid, r, ff, kind_now == RAY_OWN_SHADOW || kind_now == RAY_FOREIGN);
-            if (fresh) path_begin<COUNT>(a, occl, ra, rb, r, busy, fin, s_stack, stack_ovf, tid, gtid, c);
+            if (fresh) {
+                busy = path_begin<COUNT>(a, occl, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
+                fin = !busy;
+            }
         }
         if (COUNT) {
             const unsigned long long t = wall_clock64();
@@ -2244,42 +2105,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         }
         if (COUNT) p_tl += wall_clock64() - p_t;
     }
-    if (COUNT) {
-        if (__lane_id() == 0 && pa.prof) {
-            const unsigned long long tot = wall_clock64() - p_t0;
-            PathProfile &q = *pa.prof;
-            atomicAdd(&q.waves, 1ull);
-            atomicAdd(&q.outer, p_outer);
-            atomicAdd(&q.procs, p_procs);
-            atomicAdd(&q.trav_iters, c.iters);
-            atomicAdd(&q.t_proc, p_tp);
-            atomicAdd(&q.t_trav, p_tt);
-            atomicAdd(&q.t_leaf, p_tl);
-            atomicAdd(&q.t_total, tot);
-            atomicMax(&q.t_max, tot);
-            atomicAdd(&q.lanes_proc, p_lanes);
-            atomicAdd(&q.t_shade, p_tsh);
-        }
-        const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
-        for (int m = 0; m < 2; m++) {
-            const unsigned long long rr = wave_sum(c.rays[m]), b = wave_sum(c.box[m]), t = wave_sum(c.tri[m]),
-                                     v = wave_sum(c.visit[m]), dp = wave_sum(c.deep[m]);
-            if (__lane_id() == 0) {
-                TraceCounters &tc = a.counters[slot_of[m]];
-                atomicAdd(&tc.rays, rr);
-                atomicAdd(&tc.box, b);
-                atomicAdd(&tc.tri, t);
-                atomicAdd(&tc.visits, v);
-                atomicAdd(&tc.deep, dp);
-            }
-        }
-        const unsigned long long st = wave_sum(c.strav), sl = wave_sum(c.sleaf), sr = wave_sum(c.stri);
-        if (__lane_id() == 0) {
-            atomicAdd(&a.counters[TRACE_CLOSEST].slots_trav, st);
-            atomicAdd(&a.counters[TRACE_CLOSEST].slots_leaf, sl);
-            atomicAdd(&a.counters[TRACE_CLOSEST].slots_tri, sr);
-        }
-    }
+    if (COUNT) path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
 }
 
 // Film::merge_tile (core/film.h:85-95) on the device: a context's packed film (one float4 per
