@@ -237,10 +237,11 @@ struct akr_hip_ctx {
     uint32_t path_grid = 0;   // resident workgroups of the persistent path kernel
     uint32_t path_grid_defer = 0;  // ... of its deferred-NEE form
     // option "path_defer": 1 = k_path_defer (max_depth <= 8), 0 = k_path, 2 (default) = k_path_defer for
-    // renders of at most path_defer_pixels pixels (measured on C3, DESIGN.md §3.9: 7 % faster on an
-    // 8-way share, slower on 4-way and larger shares, whose lanes seldom have spare capacity)
+    // renders of at most path_defer_pixels pixels (measured on C3, DESIGN.md §3.9: 13 % faster on an
+    // 8-way share and 4 % on a 4-way one, 1 % slower on a 2-way share and 5 % on the whole frame,
+    // whose lanes seldom have spare capacity)
     int path_defer = 2;
-    int64_t path_defer_pixels = 400000;
+    int64_t path_defer_pixels = 600000;
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     DBuf<float4> d_contrib;   // k_path_defer: per-lane NEE contributions awaiting their shadow result
     // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the

@@ -1065,6 +1065,17 @@ __device__ __forceinline__ float mat_x(const SceneDev &s, float c, int32_t img, 
     return img < 0 ? c : tex_eval(s, img, tc).x;
 }
 
+// Scene::select_light's index: upper_bound over the light CDF (distribution.h:32-44), clamped
+__device__ __forceinline__ int select_light_index(const SceneDev &s, float x) {
+    int lo = 0, hi = s.n_lights + 1;
+    while (lo < hi) {
+        const int m = (lo + hi) / 2;
+        if (s.light_cdf[m] <= x) lo = m + 1; else hi = m;
+    }
+    const int li = hi - 1;
+    return li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
+}
+
 __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
                                           uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
     o.emit = o.ext = o.sh = false;
@@ -1134,14 +1145,7 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     // select_light(sampler.next2d()) — scene.h:79-90
     const V2 su = lcg_next2(seed);
     if (s.n_lights > 0) {
-        int lo = 0, hi = s.n_lights + 1;  // upper_bound, distribution.h:32-44
-        while (lo < hi) {
-            const int m = (lo + hi) / 2;
-            if (s.light_cdf[m] <= su.x) lo = m + 1; else hi = m;
-        }
-        int li = hi - 1;
-        li = li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
-        const AKR_GLOBAL LightDev &lt = s.lights[li];
+        const AKR_GLOBAL LightDev &lt = s.lights[select_light_index(s, su.x)];
         const V2 lu = lcg_next2(seed);
         // AreaLight::sample (light.h:58-71); lng, the area and the selection pdf are precomputed
         const float su0 = sqrtf(lu.x);
