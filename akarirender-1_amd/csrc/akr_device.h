@@ -119,6 +119,7 @@ struct SceneDev {
     const AKR_GLOBAL LightDev *lights;
     const AKR_GLOBAL float *light_cdf;  // n_lights + 1
     int32_t n_lights;
+    int32_t n_mats;
 };
 
 struct CameraDev {

@@ -195,6 +195,7 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_mesh_base;
     float func_int = 0;
     int32_t n_lights = 0;
+    int32_t n_mats = 0;
     bool has_image_tex = false;
     bool simple_shading = true;  // every material Diffuse / Emissive with constant textures
 
@@ -234,8 +235,7 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
-    uint32_t path_grid = 0;   // resident workgroups of the persistent path kernel
-    uint32_t path_grid_defer = 0;  // ... of its deferred-NEE form
+    uint32_t path_grid[2][2] = {{0, 0}, {0, 0}};  // resident workgroups of the persistent path kernels [defer][tab]
     // option "path_defer": 1 = k_path_defer (max_depth <= 8), 0 = k_path, 2 (default) = k_path_defer for
     // renders of at most path_defer_pixels pixels (measured on C3, DESIGN.md §3.9: 13 % faster on an
     // 8-way share and 4 % on a 4-way one, 1 % slower on a 2-way share and 5 % on the whole frame,
@@ -243,6 +243,7 @@ struct akr_hip_ctx {
     int path_defer = 2;
     int64_t path_defer_pixels = 600000;
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
+    bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
     DBuf<float4> d_contrib;   // k_path_defer: per-lane NEE contributions awaiting their shadow result
     // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the
     // render has at most path_auto_pixels pixels (default: any size; measured on C3, DESIGN.md §3.8,
@@ -356,6 +357,7 @@ struct akr_hip_ctx {
         s.lights = (decltype(s.lights))d_lights.p;
         s.light_cdf = (decltype(s.light_cdf))d_cdf.p;
         s.n_lights = n_lights;
+        s.n_mats = n_mats;
         return s;
     }
 
@@ -428,6 +430,7 @@ struct akr_hip_ctx {
             if (x.type == AKR_MAT_MIX) resolve(x.fraction, &d.frac, 1, d.frac_img);
         }
         d_mats.upload(md.data(), md.size(), stream);
+        n_mats = (int32_t)md.size();
         std::vector<TexDev> td(texs.size());
         for (size_t k = 0; k < texs.size(); k++) {
             const akr_texture &t = texs[k];
@@ -504,9 +507,11 @@ struct akr_hip_ctx {
             trace_grid[m] = (uint32_t)(n_cu * trace_blocks_per_cu(m));
             mx = std::max(mx, trace_grid[m]);
         }
-        path_grid = (uint32_t)(n_cu * path_blocks_per_cu(false));
-        path_grid_defer = (uint32_t)(n_cu * path_blocks_per_cu(true));
-        mx = std::max(mx, std::max(path_grid, path_grid_defer));
+        for (int d = 0; d < 2; d++)
+            for (int t = 0; t < 2; t++) {
+                path_grid[d][t] = (uint32_t)(n_cu * path_blocks_per_cu(d != 0, t != 0));
+                mx = std::max(mx, path_grid[d][t]);
+            }
         ovf_threads = mx * kTraceBlock;
         d_ovf.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
         d_ovf_side.reserve((size_t)ovf_threads * (kStackMax - kStackLds));
@@ -813,7 +818,9 @@ struct akr_hip_ctx {
                 pa.prof = count ? d_pprof.p : nullptr;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
-                const uint64_t resident = (uint64_t)(defer ? path_grid_defer : path_grid) * (uint64_t)path_grid_pct / 100;
+                // the shading's material / light / CDF tables in LDS when they fit
+                const bool tab = path_tab && path_tab_fits(n_mats, n_lights);
+                const uint64_t resident = (uint64_t)path_grid[defer][tab] * (uint64_t)path_grid_pct / 100;
                 const uint32_t grid = (uint32_t)std::max<uint64_t>(
                     1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
                 if (defer) {
@@ -821,7 +828,7 @@ struct akr_hip_ctx {
                     pa.contrib = d_contrib.p;
                     pa.mix = path_mix ? 1u : 0u;
                 }
-                timed("path", ms, [&] { launch_path(count, defer, pa, grid, ms); });
+                timed("path", ms, [&] { launch_path(count, defer, tab, pa, grid, ms); });
                 HIPCHK(hipGetLastError());
             }
             last_passes = 1;
@@ -1111,6 +1118,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_defer_pixels = value;
         } else if (k == "path_mix") {
             ctx->path_mix = value != 0;
+        } else if (k == "path_tab") {
+            ctx->path_tab = value != 0;
         } else if (k == "path_grid_pct") {
             if (value < 1 || value > 100) throw std::runtime_error("path_grid_pct must be in [1, 100]");
             ctx->path_grid_pct = (int)value;

@@ -1041,7 +1041,8 @@ __device__ __forceinline__ V3 tex_eval(const SceneDev &s, int32_t ti, V2 tc) {
     return v3(p[0], p[1], p[2]);
 }
 
-__device__ __forceinline__ V3 ld3(const float *p) { return v3(p[0], p[1], p[2]); }
+template <class P>  // a float pointer in any address space (global scene arrays, LDS tables)
+__device__ __forceinline__ V3 ld3(P p) { return v3(p[0], p[1], p[2]); }
 
 // One bounce of GenericPathTracer::run_megakernel at a closest hit (pathtracer.h:137-162):
 // on_surface_scatter (:96-132) then compute_direct_lighting(select_light) (:65-91).  Shared by the
@@ -1058,26 +1059,83 @@ struct Bounce {
 };
 
 // Material channel: the resolved constant, or the image texture's texel
-__device__ __forceinline__ V3 mat_rgb(const SceneDev &s, const float (&c)[3], int32_t img, V2 tc) {
+template <class C>  // float[3] in any address space
+__device__ __forceinline__ V3 mat_rgb(const SceneDev &s, const C &c, int32_t img, V2 tc) {
     return img < 0 ? v3(c[0], c[1], c[2]) : tex_eval(s, img, tc);
 }
 __device__ __forceinline__ float mat_x(const SceneDev &s, float c, int32_t img, V2 tc) {
     return img < 0 ? c : tex_eval(s, img, tc).x;
 }
 
+// The shading's small per-scene tables (materials, lights, light CDF) behind one accessor: read
+// from HBM (GlobalTab), or from an LDS copy that the persistent path kernels make at launch when the
+// tables fit kTabBytes (LdsTab).  A processing phase's material -> CDF -> light chain of dependent
+// loads then waits on LDS instead of L2/HBM.  Same values, same arithmetic.
+#define AKR_LDS __attribute__((address_space(3)))
+constexpr uint32_t kTabBytes = 1024;
+struct GlobalTab {
+    const AKR_GLOBAL MatDev *mats;
+    const AKR_GLOBAL LightDev *lights;
+    const AKR_GLOBAL float *cdf;
+    __device__ const AKR_GLOBAL MatDev *mat(int i) const { return mats + i; }
+    __device__ const AKR_GLOBAL LightDev *light(int i) const { return lights + i; }
+    __device__ float cdf_at(int i) const { return cdf[i]; }
+};
+struct LdsTab {
+    const AKR_LDS MatDev *mats;
+    const AKR_LDS LightDev *lights;
+    const AKR_LDS float *cdf;
+    __device__ const AKR_LDS MatDev *mat(int i) const { return mats + i; }
+    __device__ const AKR_LDS LightDev *light(int i) const { return lights + i; }
+    __device__ float cdf_at(int i) const { return cdf[i]; }
+};
+__host__ __device__ constexpr uint32_t tab_bytes(uint32_t n_mats, uint32_t n_lights) {
+    return n_lights * (uint32_t)sizeof(LightDev) + n_mats * (uint32_t)sizeof(MatDev) + (n_lights + 1) * 4u;
+}
+static_assert(sizeof(LightDev) % 16 == 0 && sizeof(MatDev) % 16 == 0, "LDS table records stay 16-B aligned");
+bool path_tab_fits(int32_t n_mats, int32_t n_lights) {
+    return n_mats >= 0 && n_lights >= 0 && n_mats <= 64 && n_lights <= 64 &&
+           tab_bytes((uint32_t)n_mats, (uint32_t)n_lights) <= kTabBytes;
+}
+__device__ __forceinline__ GlobalTab global_tab(const SceneDev &s) { return GlobalTab{s.mats, s.lights, s.light_cdf}; }
+
+// TAB: the workgroup copies the tables into `buf` (lights, materials, CDF; one barrier at launch)
+template <bool TAB> struct PathTab;
+template <> struct PathTab<false> {
+    static __device__ __forceinline__ GlobalTab make(const SceneDev &s, uint4 *) { return global_tab(s); }
+};
+template <> struct PathTab<true> {
+    static __device__ __forceinline__ LdsTab make(const SceneDev &s, uint4 *buf) {
+        AKR_LDS uint32_t *d = (AKR_LDS uint32_t *)buf;
+        const uint32_t wl = (uint32_t)s.n_lights * (uint32_t)(sizeof(LightDev) / 4);
+        const uint32_t wm = (uint32_t)s.n_mats * (uint32_t)(sizeof(MatDev) / 4);
+        const uint32_t wc = s.n_lights > 0 ? (uint32_t)s.n_lights + 1 : 0u;
+        const AKR_GLOBAL uint32_t *gl = (const AKR_GLOBAL uint32_t *)s.lights;
+        const AKR_GLOBAL uint32_t *gm = (const AKR_GLOBAL uint32_t *)s.mats;
+        const AKR_GLOBAL uint32_t *gc = (const AKR_GLOBAL uint32_t *)s.light_cdf;
+        for (uint32_t i = threadIdx.x; i < wl; i += blockDim.x) d[i] = gl[i];
+        for (uint32_t i = threadIdx.x; i < wm; i += blockDim.x) d[wl + i] = gm[i];
+        for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) d[wl + wm + i] = gc[i];
+        __syncthreads();
+        return LdsTab{(const AKR_LDS MatDev *)(d + wl), (const AKR_LDS LightDev *)d, (const AKR_LDS float *)(d + wl + wm)};
+    }
+};
+
 // Scene::select_light's index: upper_bound over the light CDF (distribution.h:32-44), clamped
-__device__ __forceinline__ int select_light_index(const SceneDev &s, float x) {
+template <class Tab>
+__device__ __forceinline__ int select_light_index(const SceneDev &s, const Tab &tab, float x) {
     int lo = 0, hi = s.n_lights + 1;
     while (lo < hi) {
         const int m = (lo + hi) / 2;
-        if (s.light_cdf[m] <= x) lo = m + 1; else hi = m;
+        if (tab.cdf_at(m) <= x) lo = m + 1; else hi = m;
     }
     const int li = hi - 1;
     return li < 0 ? 0 : (li > s.n_lights - 1 ? s.n_lights - 1 : li);
 }
 
-__device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
-                                          uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
+template <class Tab>
+__device__ __forceinline__ void shade_hit_tab(const SceneDev &s, const Tab &tab, uint32_t gid, float u, float v, V3 wo,
+                                              V3 beta, uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
     o.emit = o.ext = o.sh = false;
     const ShadeTri tr = s.tri[gid];
     const int32_t mid = (int32_t)fbits(tr.a.w);
@@ -1092,7 +1150,7 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
         const AKR_GLOBAL float *tt = s.texcoords + 6 * (size_t)gid;
         tc = lerp3(V2{tt[0], tt[1]}, V2{tt[2], tt[3]}, V2{tt[4], tt[5]}, u, v);
     }
-    const AKR_GLOBAL MatDev *mat = &s.mats[mid];
+    auto mat = tab.mat(mid);
     if (mat->type == AKR_MAT_EMISSIVE) {
         if (depth == 0) {
             const bool face_front = dot(neg(wo), ng) < 0.0f;
@@ -1112,11 +1170,11 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
         const float frac = mat_x(s, mat->frac, mat->frac_img, tc);
         if (sel_u < frac) {
             sel_u = sel_u / frac;
-            mat = &s.mats[mat->second];
+            mat = tab.mat(mat->second);
             choice_pdf *= 1.0f / frac;
         } else {
             sel_u = (sel_u - frac) / (1.0f - frac);
-            mat = &s.mats[mat->first];
+            mat = tab.mat(mat->first);
             choice_pdf *= 1.0f / (1.0f - frac);
         }
     }
@@ -1145,7 +1203,7 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     // select_light(sampler.next2d()) — scene.h:79-90
     const V2 su = lcg_next2(seed);
     if (s.n_lights > 0) {
-        const AKR_GLOBAL LightDev &lt = s.lights[select_light_index(s, su.x)];
+        const auto &lt = *tab.light(select_light_index(s, tab, su.x));
         const V2 lu = lcg_next2(seed);
         // AreaLight::sample (light.h:58-71); lng, the area and the selection pdf are precomputed
         const float su0 = sqrtf(lu.x);
@@ -1183,6 +1241,11 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
         o.e0 = make_float4(p.x, p.y, p.z, kEps / cng);
         o.e1 = make_float4(wi.x, wi.y, wi.z, kInf);
     }
+}
+
+__device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float u, float v, V3 wo, V3 beta,
+                                          uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
+    shade_hit_tab(s, global_tab(s), gid, u, v, wo, beta, seed, depth, max_depth, last, o);
 }
 
 // Out-of-line copy for the persistent path kernels (build option AKR_PATH_CALL_SHADE): a call keeps the
@@ -1579,11 +1642,12 @@ __device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &
 // spilled without this); the waiting lanes read their finished ray's result from the same place.
 constexpr int kParkFields = 12;  // o.xyz d.xyz tmin tmax best u v gid | cur | sp
 
-template <bool COUNT>
+template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path(PathArgs pa) {
     const TraceArgs &a = pa.t;
     __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
     __shared__ uint32_t s_park[kParkFields + 2][kTraceBlock];
+    __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
@@ -1591,6 +1655,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const uint32_t n = pa.n_pix;
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
     const bool ff = a.any_far_first != 0;
+    const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -1660,7 +1725,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #ifdef AKR_PROBE_NOSHADE  // timing probe only: no shading
                     bo.emit = false; bo.sh = false; bo.ext = hgid & 1; bo.e0 = make_float4(wo.x, wo.y, wo.z, 1.f); bo.e1 = bo.e0; bo.nb = wo;
 #elif !defined(AKR_PATH_CALL_SHADE)  // inlined (default): 3 % faster than the out-of-line call once every load is global
-                    shade_hit(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
+                    shade_hit_tab(pa.sc, tab, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
                               pa.max_depth, depth == nb - 1, bo);
 #else
                     shade_hit_call(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
@@ -1835,11 +1900,12 @@ struct DeferState {
     __device__ __forceinline__ bool running() const { return get(RUN, 1) != 0; }
 };
 
-template <bool COUNT>
+template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_defer(PathArgs pa) {
     const TraceArgs &a = pa.t;
     __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
     __shared__ uint32_t s_park[kParkFields + 2][kTraceBlock];
+    __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
     __shared__ uint32_t s_res[kTraceBlock];  // per owner lane: resolved bit (slot), occluded bit (16 + slot)
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
@@ -1850,6 +1916,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const uint32_t n = pa.n_pix;
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;
     const bool ff = a.any_far_first != 0;
+    const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -1932,7 +1999,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         const int depth = s.depth();
                         Bounce bo;
 #ifndef AKR_PATH_CALL_SHADE  // inlined (default): 3 % faster than the out-of-line call once every load is global
-                        shade_hit(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
+                        shade_hit_tab(pa.sc, tab, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
                                   pa.max_depth, depth == nb - 1, bo);
 #else
                         shade_hit_call(pa.sc, hgid, bitsf(s_park[9][tid]), bitsf(s_park[10][tid]), wo, beta, seed, depth,
@@ -2235,20 +2302,31 @@ void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     hipLaunchKernelGGL(k_splat, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
-void launch_path(bool count, bool defer, const PathArgs &a, uint32_t grid, hipStream_t st) {
+template <bool COUNT, bool TAB>
+static void launch_path_t(bool defer, const PathArgs &a, uint32_t grid, hipStream_t st) {
+    if (defer) hipLaunchKernelGGL((k_path_defer<COUNT, TAB>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+    else hipLaunchKernelGGL((k_path<COUNT, TAB>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+}
+void launch_path(bool count, bool defer, bool tab, const PathArgs &a, uint32_t grid, hipStream_t st) {
     if (grid == 0) return;
-    if (defer) {
-        if (count) hipLaunchKernelGGL(k_path_defer<true>, dim3(grid), dim3(kTraceBlock), 0, st, a);
-        else hipLaunchKernelGGL(k_path_defer<false>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+    if (tab && !path_tab_fits(a.sc.n_mats, a.sc.n_lights)) tab = false;  // the LDS copy must hold every record
+    if (count) {
+        if (tab) launch_path_t<true, true>(defer, a, grid, st);
+        else launch_path_t<true, false>(defer, a, grid, st);
     } else {
-        if (count) hipLaunchKernelGGL(k_path<true>, dim3(grid), dim3(kTraceBlock), 0, st, a);
-        else hipLaunchKernelGGL(k_path<false>, dim3(grid), dim3(kTraceBlock), 0, st, a);
+        if (tab) launch_path_t<false, true>(defer, a, grid, st);
+        else launch_path_t<false, false>(defer, a, grid, st);
     }
 }
-int path_blocks_per_cu(bool defer) {
+int path_blocks_per_cu(bool defer, bool tab) {
     int nb = 0;
-    const hipError_t e = defer ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_defer<false>, kTraceBlock, 0)
-                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false>, kTraceBlock, 0);
+    hipError_t e;
+    if (defer)
+        e = tab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_defer<false, true>, kTraceBlock, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_defer<false, false>, kTraceBlock, 0);
+    else
+        e = tab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false, true>, kTraceBlock, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false, false>, kTraceBlock, 0);
     if (e != hipSuccess || nb <= 0) nb = 1;
     return nb;
 }

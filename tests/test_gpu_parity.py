@@ -475,21 +475,32 @@ def test_auto_form_by_shading(hip_ctx_factory):
                 assert set(ctx.kernel_stats()) == {want}, (sc, complex_ok, ctx.kernel_stats())
 
 
-@pytest.mark.parametrize("path,defer,mix", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)])
-def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix):
+def _tab_fits(cs):
+    """The persistent kernels' LDS copy of the scene tables holds the scene (kernels.hip kTabBytes:
+    96-B lights, 48-B materials, the light CDF)."""
+    nl, nm = len(cs.lights), len(cs.materials)
+    return nl * 96 + nm * 48 + (nl + 1) * 4 <= 1024
+
+
+@pytest.mark.parametrize("path,defer,mix,tab", [(0, 0, 0, 1), (1, 0, 0, 0), (1, 0, 0, 1), (1, 1, 0, 1),
+                                                (1, 1, 1, 0), (1, 1, 1, 1)])
+def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
     §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
     scrambled or tile-order pixel fetch) and the wavefront kernels give the oracle's image bit for
     bit: ragged / clipped / empty tiles, depths 0-9 (above 8 the deferred form falls back to
     k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
-    deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes)."""
+    deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes); with the
+    scene's material / light / CDF tables read from HBM or from the kernels' LDS copy (tab)."""
     def opts(ctx):
         ctx.set_option("path", path)
         ctx.set_option("path_defer", defer)
         ctx.set_option("path_mix", mix)
+        ctx.set_option("path_tab", tab)
     with hip_ctx_factory(0) as ctx:
         opts(ctx)
         cs, orc = _setup(ctx, cornell((40, 24)))
+        assert _tab_fits(cs)
         tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]
         for spp, depth in ((3, 0), (2, 1), (3, 2), (5, 5), (3, 8), (2, 9)):
             _check_render(ctx, orc, spp, depth, tiles, 40, 24)
@@ -499,6 +510,7 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
         with hip_ctx_factory(0) as ctx:   # one scene per context (uploads append meshes)
             opts(ctx)
             cs, orc = _setup(ctx, sc)
+            assert _tab_fits(cs)
             W, H = cs.camera.resolution
             _check_render(ctx, orc, 5, 5, [(0, 0, W, H)], W, H)
             _check_render(ctx, orc, 9, 3, [(0, 0, W, H)], W, H)
