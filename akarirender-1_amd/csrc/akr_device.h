@@ -32,12 +32,12 @@ constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 #endif
 constexpr int kTraceBlock = AKR_TRACE_BLOCK;  // threads per traversal workgroup (the LDS stack's row)
 #ifndef AKR_STACK_LDS
-#define AKR_STACK_LDS 12
+#define AKR_STACK_LDS 15
 #endif
 #ifndef AKR_REFILL_MIN
 #define AKR_REFILL_MIN 32
 #endif
-constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entries per ray (8 B each)
+constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entries per ray (8 B each; 15 fill the LDS left by the path kernels' park area)
 constexpr int kStackMax = 96;         // >= 3 pushes x 32 wide levels (BVH2 depth <= 64)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle
