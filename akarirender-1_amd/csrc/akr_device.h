@@ -290,6 +290,7 @@ struct PathArgs {
     float4 *contrib;               // k_path_defer: per lane, [18][lanes]: 16 NEE contributions awaiting their
                                    // shadow result (parity * 8 + bounce), then the waiting extension ray
     uint32_t mix;                  // k_path_defer: scrambled pixel order within each XCD shard
+    const uint32_t *order;         // optional: fetch index -> slot (cost-ordered fetch)
 };
 
 }  // namespace akr

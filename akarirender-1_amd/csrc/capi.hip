@@ -244,6 +244,16 @@ struct akr_hip_ctx {
     int64_t path_defer_pixels = 600000;
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
+    // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
+    // ranks the pixels, and each XCD shard hands out its costliest pixels first, so a launch ends on
+    // cheap ones.  1 (default) = k_path, 2 = k_path and k_path_defer, 0 = off; renders of at least
+    // path_order_min_spp samples only; classes of 2^path_order_shift pilot steps
+    int path_order = 1;
+    int path_order_min_spp = 16;
+    int path_order_shift = 2;
+    DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
+    DBuf<uint8_t> d_otmp;
+    DBuf<TraceCounters> d_ocnt;
     DBuf<float4> d_contrib;   // k_path_defer: per-lane NEE contributions awaiting their shadow result
     // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the
     // render has at most path_auto_pixels pixels (default: any size; measured on C3, DESIGN.md §3.8,
@@ -625,6 +635,33 @@ struct akr_hip_ctx {
         mark_done(st);
     }
 
+    // Cost-ordered pixel fetch: d_oidx[1] = the slots of each XCD shard in order of
+    // decreasing pilot cost (tile order within a cost class).  The pilot traces the camera ray of
+    // every slot's first sample with the counting kernel into scratch counters; nothing it does
+    // reaches the film, the sampler states or the context's statistics.
+    void pixel_order(uint32_t N, hipStream_t ms) {
+        for (int k = 0; k < 2; k++) {
+            d_okey[k].reserve(N);
+            d_oidx[k].reserve(N);
+        }
+        d_owork.reserve(kTraceWords);
+        d_ocnt.reserve(3);
+        const size_t tb = pixel_order_tmp_bytes(N);
+        d_otmp.reserve(tb);
+        HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
+        launch_pilot_rays(cam, d_pixel.p, N, d_ray0.p, ms);
+        TraceArgs t = trace_args(d_owork.p);
+        t.rays = d_ray0.p;
+        t.n = N;
+        t.hits = d_hit.p;
+        t.counters = d_ocnt.p;
+        t.ray_steps = d_okey[1].p;
+        launch_trace(TRACE_CLOSEST, true, true, true, t, grid_for(TRACE_CLOSEST, N), ms);
+        launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, d_okey[0].p, d_oidx[0].p, ms);
+        sort_pixel_order(d_otmp.p, tb, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
+        HIPCHK(hipGetLastError());
+    }
+
     // Pixels of the tile list (tiles in order, row-major inside a tile) into h_pixel / d_pixel;
     // sizes the queues and the per-pass counter sets.  Returns the pixel count.
     // look_ok: the render may use lookahead lanes (cur_look); the path buffers are sized for it.
@@ -827,6 +864,10 @@ struct akr_hip_ctx {
                     d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
                     pa.contrib = d_contrib.p;
                     pa.mix = path_mix ? 1u : 0u;
+                }
+                if (path_order != 0 && (!defer || path_order == 2) && p.spp >= path_order_min_spp && N >= 2) {
+                    timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
+                    pa.order = d_oidx[1].p;
                 }
                 timed("path", ms, [&] { launch_path(count, defer, tab, pa, grid, ms); });
                 HIPCHK(hipGetLastError());
@@ -1116,6 +1157,15 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_defer_pixels") {
             if (value < 0) throw std::runtime_error("path_defer_pixels must be >= 0");
             ctx->path_defer_pixels = value;
+        } else if (k == "path_order") {
+            if (value < 0 || value > 2) throw std::runtime_error("path_order must be 0, 1 or 2");
+            ctx->path_order = (int)value;
+        } else if (k == "path_order_min_spp") {
+            if (value < 0) throw std::runtime_error("path_order_min_spp must be >= 0");
+            ctx->path_order_min_spp = (int)std::min<int64_t>(value, INT32_MAX);
+        } else if (k == "path_order_shift") {
+            if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
+            ctx->path_order_shift = (int)value;
         } else if (k == "path_mix") {
             ctx->path_mix = value != 0;
         } else if (k == "path_tab") {

@@ -1555,8 +1555,8 @@ struct PixelFetch {
     int shards_left;
     bool drained;
 };
-__device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t *work, bool mix, bool &need,
-                                             bool &done, uint32_t &pix) {
+__device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t *work, bool mix,
+                                             const uint32_t *order, bool &need, bool &done, uint32_t &pix) {
     while (true) {
         const unsigned long long want = __ballot(need && !done);
         if (want == 0) break;
@@ -1573,7 +1573,8 @@ __device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t
             const uint32_t my = base + lane_prefix(want);
             const uint32_t len = f.s_hi - f.s_lo;
             if (base < len && my < len) {
-                pix = f.s_lo + (mix ? (uint32_t)(((uint64_t)my * 2147483647ull) % len) : my);
+                const uint32_t at = f.s_lo + (mix ? (uint32_t)(((uint64_t)my * 2147483647ull) % len) : my);
+                pix = order ? order[at] : at;
                 need = false;
             }
         }
@@ -1776,7 +1777,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             }
             // next pixel for the lanes that finished theirs: one atomic per wave per attempt
             const bool asked = need_pixel && !done;
-            fetch_pixels(f, n, pa.work, false, need_pixel, done, pix);
+            fetch_pixels(f, n, pa.work, false, pa.order, need_pixel, done, pix);
             if (asked && !need_pixel) {
                 const uint32_t px = pa.pixel[pix];
                 left = pa.spp;
@@ -2073,7 +2074,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 need_pixel = true;
             }
             const bool asked = need_pixel && !done;
-            fetch_pixels(f, n, pa.work, pa.mix != 0, need_pixel, done, pix);
+            fetch_pixels(f, n, pa.work, pa.mix != 0, pa.order, need_pixel, done, pix);
             if (asked && !need_pixel) {
                 pxy = pa.pixel[pix];
                 left = pa.spp;
@@ -2210,6 +2211,35 @@ __global__ __launch_bounds__(kBlock) void k_check_weights(const float4 *film, ui
     if (__lane_id() == 0 && m) atomicAdd(bad, (uint32_t)__popcll(m));
 }
 
+// Cost-ordered pixel fetch of the persistent path kernels.  Pilot: the camera ray
+// of each slot's first sample, made from a copy of its seed (nothing is committed), traced by the
+// counting kernel, whose per-ray steps (traversal iterations + triangle tests) rank the pixels.
+__global__ __launch_bounds__(kBlock) void k_pilot_rays(CameraDev cam, const uint32_t *pixel, uint32_t n, float4 *rays) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t px = pixel[i];
+    const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
+    uint32_t seed = (uint32_t)(x + y * cam.width);
+    float4 r0, r1;
+    camera_ray(cam, x, y, seed, r0, r1);
+    rays[2 * (size_t)i] = r0;
+    rays[2 * (size_t)i + 1] = r1;
+}
+
+// Sort key of slot i: its XCD shard above its cost class (steps >> shift, capped, descending), so a
+// stable sort orders each shard by decreasing cost and keeps tile order within a class.
+__global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t *key,
+                                                       uint32_t *idx) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint32_t sh = 0;
+    for (uint32_t k = 1; k < kWorkShards; k++) sh += i >= shard_begin(n, k) ? 1u : 0u;
+    const uint32_t s = steps[i];  // 0xFFFFFFFF: traced by the exact BVH2 walk (rare): costliest class
+    const uint32_t cls = s == 0xFFFFFFFFu ? kOrderClassMask : min(s >> shift, kOrderClassMask);
+    key[i] = (sh << kOrderClassBits) | (kOrderClassMask - cls);
+    idx[i] = i;
+}
+
 // one word from device memory into mapped host memory (the host polls it after an event)
 __global__ void k_store_word(const uint32_t *src, uint32_t *dst) {
     if (threadIdx.x == 0) {
@@ -2333,6 +2363,14 @@ void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t
                        float *rad, float *w, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_merge_film, dim3(blocks_for(n)), dim3(kBlock), 0, st, film, pixel, order, n, width, rad, w);
+}
+void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, float4 *rays, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_pilot_rays, dim3(blocks_for(n)), dim3(kBlock), 0, st, cam, pixel, n, rays);
+}
+void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t *key, uint32_t *idx, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift, key, idx);
 }
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
     if (n == 0) return;

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include "kernels.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -353,6 +355,21 @@ void build_lbvh_gpu(const BvhInput &in, BvhOutput &out, hipStream_t st) {
         throw std::runtime_error("lbvh: tree deeper than " + std::to_string(AKR_BVH_MAX_DEPTH) +
                                  " levels (use the SAH builder for this scene)");
     out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Stable sort of the cost-ordered fetch's (shard, class) keys with their slot indices.
+size_t pixel_order_tmp_bytes(uint32_t n) {
+    size_t bytes = 0;
+    LB_CHECK(rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                       (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0,
+                                       (int)(kOrderClassBits + 3), (hipStream_t)0));
+    return bytes;
+}
+void sort_pixel_order(void *tmp, size_t tmp_bytes, const uint32_t *key_in, uint32_t *key_out, const uint32_t *idx_in,
+                      uint32_t *idx_out, uint32_t n, hipStream_t st) {
+    static_assert(kWorkShards <= 8, "the sort key holds the shard in 3 bits");
+    LB_CHECK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_in, key_out, idx_in, idx_out, n, 0,
+                                       (int)(kOrderClassBits + 3), st));
 }
 
 }  // namespace akr

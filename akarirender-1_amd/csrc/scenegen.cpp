@@ -11,6 +11,8 @@
 #include <thread>
 #include <vector>
 
+#include "bvh_build.h"
+
 namespace {
 struct Pcg {
     uint64_t state;
@@ -62,11 +64,11 @@ int akr_gen_soup(uint64_t n, uint64_t seed, float r, float *vertices, float *nor
     int T = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
     if (T < 1) T = 1;
     uint64_t chunk = (n + T - 1) / T;
-    std::vector<std::thread> ts;
-    for (int t = 0; t < T; t++) {
-        uint64_t b = t * chunk, e = std::min<uint64_t>(n, b + chunk);
-        if (b >= e) break;
-        ts.emplace_back([=] {
+    // every started thread is joined even if creating a later one fails (bvh_build.h run_on_threads)
+    akr::run_on_threads(T, [&](int t) {
+        const uint64_t b = (uint64_t)t * chunk, e = std::min<uint64_t>(n, b + chunk);
+        if (b >= e) return;
+        {
             Pcg p;
             p.state = lcg_jump(p0.state, 12 * b);
             for (uint64_t i = b; i < e; i++) {
@@ -84,9 +86,8 @@ int akr_gen_soup(uint64_t n, uint64_t seed, float r, float *vertices, float *nor
                     texcoords[6 * i + 2 * j + 1] = (float)(j % 2 == 0);
                 }
             }
-        });
-    }
-    for (auto &t : ts) t.join();
+        }
+    });
     return 0;
 }
 

@@ -482,21 +482,26 @@ def _tab_fits(cs):
     return nl * 96 + nm * 48 + (nl + 1) * 4 <= 1024
 
 
-@pytest.mark.parametrize("path,defer,mix,tab", [(0, 0, 0, 1), (1, 0, 0, 0), (1, 0, 0, 1), (1, 1, 0, 1),
-                                                (1, 1, 1, 0), (1, 1, 1, 1)])
-def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab):
+@pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
+                                                      (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
+                                                      (1, 1, 1, 1, 0), (1, 1, 1, 1, 2)])
+def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab, order):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
     §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
     scrambled or tile-order pixel fetch) and the wavefront kernels give the oracle's image bit for
     bit: ragged / clipped / empty tiles, depths 0-9 (above 8 the deferred form falls back to
     k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
     deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes); with the
-    scene's material / light / CDF tables read from HBM or from the kernels' LDS copy (tab)."""
+    scene's material / light / CDF tables read from HBM or from the kernels' LDS copy (tab); with the
+    cost-ordered pixel fetch (order, §3.10) forced on at every spp, or off."""
     def opts(ctx):
         ctx.set_option("path", path)
         ctx.set_option("path_defer", defer)
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
+        ctx.set_option("path_order", order)
+        ctx.set_option("path_order_min_spp", 0 if order else 16)
+        ctx.set_option("path_order_shift", 0)
     with hip_ctx_factory(0) as ctx:
         opts(ctx)
         cs, orc = _setup(ctx, cornell((40, 24)))

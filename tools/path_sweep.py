@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--mix", default="1", help="scrambled pixel fetch in k_path_defer (comma list)")
     ap.add_argument("--grid-pct", default="100", help="persistent path grid, %% of resident (comma list)")
     ap.add_argument("--tab", default="1", help="scene tables in LDS (comma list)")
+    ap.add_argument("--order", default="1", help="cost-ordered pixel fetch: 0 off, 1 k_path, 2 both forms (comma list)")
+    ap.add_argument("--order-shift", default="2", help="pilot-step classes of 2^shift (comma list)")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--builder", default="sbvh")
@@ -70,10 +72,13 @@ def main():
         scene.upload_scene(ctx, cs, builder={"sah": capi.BUILDER_SAH, "sbvh": capi.BUILDER_SBVH,
                                              "lbvh": capi.BUILDER_LBVH}[args.builder], n_threads=16)
         print(f"== {Path(lib).name}: built in {time.time() - t0:.1f} s", flush=True)
-        combos = [(p, f, d, m, t) for p in (int(x) for x in args.path.split(",")) for f in (int(x) for x in args.far_first.split(","))
+        combos = [(p, f, d, m, t, o, osh) for p in (int(x) for x in args.path.split(",")) for f in (int(x) for x in args.far_first.split(","))
                   for d in (int(x) for x in args.defer.split(",")) for m in (int(x) for x in args.mix.split(","))
-                  for t in (int(x) for x in args.tab.split(","))]
-        for path, ff, dfr, mx, tab in combos:
+                  for t in (int(x) for x in args.tab.split(",")) for o in (int(x) for x in args.order.split(","))
+                  for osh in (int(x) for x in args.order_shift.split(","))]
+        for path, ff, dfr, mx, tab, order, osh in combos:
+            ctx.set_option("path_order", order)
+            ctx.set_option("path_order_shift", osh)
             ctx.set_option("path_tab", tab)
             ctx.set_option("path", path)
             ctx.set_option("any_far_first", ff)
@@ -91,7 +96,7 @@ def main():
                     ctx.render_device(args.steps, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
                     torch.cuda.synchronize(dev)
                     res.append((time.perf_counter() - t) / args.steps * 1e3)
-                print(f"   path={path} far_first={ff} defer={dfr} mix={mx} tab={tab} min_wait={mw} grid={gp}%: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
+                print(f"   path={path} far_first={ff} defer={dfr} mix={mx} tab={tab} order={order}/{osh} min_wait={mw} grid={gp}%: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
                       + "".join(f", {n}-way rank {r:.3f} ms/step (projected {res[0] / r:.2f}x, {W * H / r / 1e3:.0f} Msamples/s)"
                                 for n, r in zip(splits, res[1:])), flush=True)
                 if args.profile and path:
