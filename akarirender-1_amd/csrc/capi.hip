@@ -246,9 +246,10 @@ struct akr_hip_ctx {
     bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
     // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
     // ranks the pixels, and each XCD shard hands out its costliest pixels first, so a launch ends on
-    // cheap ones.  1 (default) = k_path, 2 = k_path and k_path_defer, 0 = off; renders of at least
-    // path_order_min_spp samples only; classes of 2^path_order_shift pilot steps
-    int path_order = 1;
+    // cheap ones (in k_path_defer it replaces the scrambled fetch).  2 (default) = both persistent
+    // kernels, 1 = k_path only, 0 = off; renders of at least path_order_min_spp samples only; classes
+    // of 2^path_order_shift pilot steps.  Measured on C3 at 64 spp: 2- / 4- / 8-way shares 2-5 % faster
+    int path_order = 2;
     int path_order_min_spp = 16;
     int path_order_shift = 2;
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;

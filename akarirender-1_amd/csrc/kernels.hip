@@ -2074,7 +2074,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 need_pixel = true;
             }
             const bool asked = need_pixel && !done;
-            fetch_pixels(f, n, pa.work, pa.mix != 0, pa.order, need_pixel, done, pix);
+            fetch_pixels(f, n, pa.work, pa.mix != 0 && !pa.order, pa.order, need_pixel, done, pix);  // the cost order replaces the scramble
             if (asked && !need_pixel) {
                 pxy = pa.pixel[pix];
                 left = pa.spp;

@@ -115,11 +115,24 @@ def test_c3_render_tile_subset_bit_exact(c3):
     # NEE runs (shadow rays are traced), though the 1-cm mean free path of the soup occludes the
     # emitter above it from everything the camera sees: the C3 frame is dark by construction
     assert st["shadow_rays"] > 0 and st["extension_rays"] > 0
+    # the cost-ordered pixel fetch (on by default from 16 spp) forced on at 2 spp,
+    # for k_path and for the deferred form this subset runs with by default
+    try:
+        for order, defer in ((1, 0), (2, 2)):
+            ctx.set_option("path_order", order)
+            ctx.set_option("path_order_min_spp", 0)
+            ctx.set_option("path_defer", defer)
+            rad2, w2 = ctx.render(2, 5, tiles, W, H)
+            assert np.array_equal(w2, ow) and np.array_equal(rad2, orad), f"path_order={order} differs"
+    finally:
+        ctx.set_option("path_order", 2)
+        ctx.set_option("path_order_min_spp", 16)
+        ctx.set_option("path_defer", 2)
 
 
 def test_c3_full_frame_split_invariance(c3):
-    """Full 1080p frame at 1 spp on the device: every pixel holds one sample (the library's in-band
-    check runs too), and rank 3's share of an 8-way tile split renders the same bits as the same
+    """Full 1080p frame at 1 spp on the device (cost-ordered fetch forced on): every pixel holds one
+    sample (the library's in-band check runs too), and rank 3's share of an 8-way tile split renders the same bits as the same
     pixels of the whole frame."""
     import torch
     ctx, cs, orc, _ = c3
@@ -127,9 +140,13 @@ def test_c3_full_frame_split_invariance(c3):
     full = dist.tile_grid(W, H, TILE)
     n = dist.n_pixels(full)
     film = torch.zeros(4 * n, device=dev)
-    ctx.render_device(1, 5, full, film[:3 * n].data_ptr(), film[3 * n:].data_ptr(),
-                      torch.cuda.current_stream(dev).cuda_stream)
-    torch.cuda.synchronize(dev)
+    ctx.set_option("path_order_min_spp", 0)  # the whole frame with the cost-ordered fetch (§3.10)
+    try:
+        ctx.render_device(1, 5, full, film[:3 * n].data_ptr(), film[3 * n:].data_ptr(),
+                          torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+    finally:
+        ctx.set_option("path_order_min_spp", 16)
     packed = film.cpu().numpy()
     assert np.all(packed[3 * n:] == 1.0)
     frame = np.zeros((H, W, 3), np.float32)

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--mix", default="1", help="scrambled pixel fetch in k_path_defer (comma list)")
     ap.add_argument("--grid-pct", default="100", help="persistent path grid, %% of resident (comma list)")
     ap.add_argument("--tab", default="1", help="scene tables in LDS (comma list)")
-    ap.add_argument("--order", default="1", help="cost-ordered pixel fetch: 0 off, 1 k_path, 2 both forms (comma list)")
+    ap.add_argument("--order", default="2", help="cost-ordered pixel fetch: 0 off, 1 k_path, 2 both forms (comma list)")
     ap.add_argument("--order-shift", default="2", help="pilot-step classes of 2^shift (comma list)")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--tris", type=int, default=10_000_000)
