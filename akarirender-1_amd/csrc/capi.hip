@@ -247,10 +247,11 @@ struct akr_hip_ctx {
     // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
     // ranks the pixels, and each XCD shard hands out its costliest pixels first, so a launch ends on
     // cheap ones (in k_path_defer it replaces the scrambled fetch).  2 (default) = both persistent
-    // kernels, 1 = k_path only, 0 = off; renders of at least path_order_min_spp samples only; classes
+    // kernels, 1 = k_path only, 0 = off; renders of at least path_order_min_spp samples only (the
+    // pilot costs about one third of a sample pass); classes
     // of 2^path_order_shift pilot steps.  Measured on C3 at 64 spp: 2- / 4- / 8-way shares 2-5 % faster
     int path_order = 2;
-    int path_order_min_spp = 16;
+    int path_order_min_spp = 64;
     int path_order_shift = 2;
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -571,6 +572,15 @@ struct akr_hip_ctx {
         d_L[0].reserve(n);
         d_L[1].reserve(n);
         d_film.reserve(n);
+        // the cost-ordered fetch's pilot buffers, with the rest: a first ordered
+        // render then allocates nothing inside the caller's timed region
+        for (int k = 0; k < 2; k++) {
+            d_okey[k].reserve(n);
+            d_oidx[k].reserve(n);
+        }
+        d_owork.reserve(kTraceWords);
+        d_ocnt.reserve(3);
+        d_otmp.reserve(pixel_order_tmp_bytes((uint32_t)std::min<size_t>(n, UINT32_MAX)));
         cap = n;
     }
 
@@ -641,14 +651,8 @@ struct akr_hip_ctx {
     // every slot's first sample with the counting kernel into scratch counters; nothing it does
     // reaches the film, the sampler states or the context's statistics.
     void pixel_order(uint32_t N, hipStream_t ms) {
-        for (int k = 0; k < 2; k++) {
-            d_okey[k].reserve(N);
-            d_oidx[k].reserve(N);
-        }
-        d_owork.reserve(kTraceWords);
-        d_ocnt.reserve(3);
-        const size_t tb = pixel_order_tmp_bytes(N);
-        d_otmp.reserve(tb);
+        const size_t tb = pixel_order_tmp_bytes(N);  // <= the capacity's (ensure_capacity)
+        if (tb > d_otmp.n || d_okey[0].n < N) throw std::runtime_error("pixel order buffers not sized");
         HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
         launch_pilot_rays(cam, d_pixel.p, N, d_ray0.p, ms);
         TraceArgs t = trace_args(d_owork.p);

@@ -126,7 +126,7 @@ def test_c3_render_tile_subset_bit_exact(c3):
             assert np.array_equal(w2, ow) and np.array_equal(rad2, orad), f"path_order={order} differs"
     finally:
         ctx.set_option("path_order", 2)
-        ctx.set_option("path_order_min_spp", 16)
+        ctx.set_option("path_order_min_spp", 64)
         ctx.set_option("path_defer", 2)
 
 
@@ -146,7 +146,7 @@ def test_c3_full_frame_split_invariance(c3):
                           torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
     finally:
-        ctx.set_option("path_order_min_spp", 16)
+        ctx.set_option("path_order_min_spp", 64)
     packed = film.cpu().numpy()
     assert np.all(packed[3 * n:] == 1.0)
     frame = np.zeros((H, W, 3), np.float32)

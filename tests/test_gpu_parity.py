@@ -500,7 +500,7 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
         ctx.set_option("path_order", order)
-        ctx.set_option("path_order_min_spp", 0 if order else 16)
+        ctx.set_option("path_order_min_spp", 0 if order else 64)
         ctx.set_option("path_order_shift", 0)
     with hip_ctx_factory(0) as ctx:
         opts(ctx)

@@ -73,7 +73,8 @@ def main(tag):
                 K, Wm = line["steps"], line["warmup"]
                 spp_total = (Wm if Wm > 0 else 0) + K + min(K, 4)
                 for k, t in traffic.items():
-                    if k.startswith("k_path") and "true" not in k and t["launches_sampled"]:
+                    # not the counting builds (k_path<true, ...>; the second argument is the LDS-table flag)
+                    if k.startswith("k_path") and "<true" not in k and t["launches_sampled"]:
                         t["hbm_bytes_per_spp"] = t["hbm_bytes_per_launch"] * t["launches_sampled"] / spp_total
     (dst / f"{tag}_traffic.json").write_text(json.dumps(
         {"tag": tag, "workload": workload, "source": f"profiles/{tag}_pmc_fetch.csv + {tag}_pmc_write.csv",
