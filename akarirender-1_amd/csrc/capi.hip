@@ -651,8 +651,10 @@ struct akr_hip_ctx {
     // every slot's first sample with the counting kernel into scratch counters; nothing it does
     // reaches the film, the sampler states or the context's statistics.
     void pixel_order(uint32_t N, hipStream_t ms) {
-        const size_t tb = pixel_order_tmp_bytes(N);  // <= the capacity's (ensure_capacity)
-        if (tb > d_otmp.n || d_okey[0].n < N) throw std::runtime_error("pixel order buffers not sized");
+        // sized for the capacity by ensure_capacity (the sort's scratch grows with n), so no size
+        // query runs per render
+        if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
+        const size_t tb = d_otmp.n;
         HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
         launch_pilot_rays(cam, d_pixel.p, N, d_ray0.p, ms);
         TraceArgs t = trace_args(d_owork.p);
