@@ -256,6 +256,7 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
     DBuf<TraceCounters> d_ocnt;
+    bool order_warm = false;
     DBuf<float4> d_contrib;   // k_path_defer: per-lane NEE contributions awaiting their shadow result
     // option "path": 1 = render with k_path, 0 = the wavefront kernels, 2 (default) = k_path when the
     // render has at most path_auto_pixels pixels (default: any size; measured on C3, DESIGN.md §3.8,
@@ -871,6 +872,12 @@ struct akr_hip_ctx {
                     d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
                     pa.contrib = d_contrib.p;
                     pa.mix = path_mix ? 1u : 0u;
+                }
+                // the first persistent render of a context runs the pilot once on a few pixels: its
+                // kernels (and rocPRIM's) are loaded then, not inside a later ordered render
+                if (path_order != 0 && !order_warm) {
+                    pixel_order((uint32_t)std::min<uint64_t>(N, 64), ms);
+                    order_warm = true;
                 }
                 if (path_order != 0 && (!defer || path_order == 2) && p.spp >= path_order_min_spp && N >= 2) {
                     timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });

@@ -198,6 +198,8 @@ def main():
     ap.add_argument("--lookahead", type=int, default=1,
                     help="speculative sample lanes per pixel (1 = off, 0 = on from --slot-target, n = at most n lanes)")
     ap.add_argument("--slot-target", type=int, default=0, help="auto lookahead: path slots per render (0: library default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -256,6 +258,9 @@ def main():
         ctx.set_option("slot_target", args.slot_target)
     if args.shadow_grid_pct != 100:
         ctx.set_option("shadow_grid_pct", args.shadow_grid_pct)
+    for kv in args.opt:
+        k, _, v = kv.partition("=")
+        ctx.set_option(k, int(v))
     log(f"[rank {rank}] {args.scene} {cs.n_tris} tris gen {t_gen:.1f}s, BVH {info.n_nodes} nodes depth {info.max_depth} "
         f"build {info.build_ms / 1e3:.1f}s sah {info.sah_cost:.1f}")
 
