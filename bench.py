@@ -34,7 +34,9 @@ RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic byte
 
 
 TRACE_KERNEL_PROF_NAME = "k_trace<0, false, true, true>"   # closest hit, uncounted, tight cull, wide (rocprof name)
-PATH_KERNEL_PROF_NAME = "k_path<false>"                      # persistent path kernel, uncounted
+# persistent path kernel, uncounted (rocprof names: <COUNT, TAB> with the LDS scene tables since r13,
+# <COUNT> before); the first one a profile holds is taken
+PATH_KERNEL_PROF_NAME = ("k_path<false, true>", "k_path<false, false>", "k_path<false>")
 
 
 def log(*a):
@@ -54,9 +56,11 @@ def measured_traffic(kernel, workload, per_spp=None):
             continue
         w = d.get("workload") or {}
         defaults = {"builder": "sah"}  # profiles written before the key existed
-        if any(w.get(k, defaults.get(k)) != v for k, v in workload.items()) or kernel not in d.get("kernels", {}):
+        names = [kernel] if isinstance(kernel, str) else list(kernel)
+        name = next((k for k in names if k in d.get("kernels", {})), None)
+        if any(w.get(k, defaults.get(k)) != v for k, v in workload.items()) or name is None:
             continue
-        rec = d["kernels"][kernel]
+        rec = d["kernels"][name]
         if per_spp is not None:   # a persistent launch renders every spp: scale the profile's per-spp bytes
             if "hbm_bytes_per_spp" not in rec:
                 continue
