@@ -267,8 +267,11 @@ struct akr_hip_ctx {
     bool path_auto_complex = false;  // option "path_auto_complex": auto also takes k_path for complex shading
     bool serial_shadow = false;  // option "serial_shadow": wavefront shadow traces on the main stream (isolated timing)
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
-    int path_min_wait = 32;
-    int path_grid_pct = 100;  // option "path_grid_pct": persistent path grid as a percentage of the resident maximum   // option "path_min_wait": k_path processes a wave's waiting lanes once this many wait
+    // option "path_min_wait": a persistent kernel's wave processes its waiting lanes once this many of
+    // 64 wait (scaled to the wave's live lanes); 0 (default) = 40 for k_path, 32 for k_path_defer
+    // (measured on C3)
+    int path_min_wait = 0;
+    int path_grid_pct = 100;  // option "path_grid_pct": persistent path grid as a percentage of the resident maximum
     DBuf<float4> d_trace_rays;
     DBuf<akr_hit> d_trace_hits;
     // akr_hip_render_node on the lead context: the frame and the staging of other contexts' films
@@ -859,7 +862,6 @@ struct akr_hip_ctx {
                 pa.spp = (uint32_t)p.spp;
                 pa.max_depth = p.max_depth;
                 pa.ray_clamp = p.ray_clamp;
-                pa.min_wait = (uint32_t)path_min_wait;
                 pa.prof = count ? d_pprof.p : nullptr;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
@@ -868,6 +870,7 @@ struct akr_hip_ctx {
                 const uint64_t resident = (uint64_t)path_grid[defer][tab] * (uint64_t)path_grid_pct / 100;
                 const uint32_t grid = (uint32_t)std::max<uint64_t>(
                     1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
+                pa.min_wait = (uint32_t)(path_min_wait > 0 ? path_min_wait : defer ? 32 : 40);
                 if (defer) {
                     d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
                     pa.contrib = d_contrib.p;
@@ -1188,7 +1191,7 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             if (value < 1 || value > 100) throw std::runtime_error("path_grid_pct must be in [1, 100]");
             ctx->path_grid_pct = (int)value;
         } else if (k == "path_min_wait") {
-            if (value < 1 || value > 64) throw std::runtime_error("path_min_wait must be in [1, 64]");
+            if (value < 0 || value > 64) throw std::runtime_error("path_min_wait must be in [0, 64] (0: per kernel)");
             ctx->path_min_wait = (int)value;
         } else if (k == "verify") {
             ctx->verify = value != 0;

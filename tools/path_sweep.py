@@ -16,7 +16,7 @@ sys.path.insert(0, str(ROOT / "akarirender-1_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", default=str(ROOT / "akarirender-1_amd" / "libakr_hip.so"))
-    ap.add_argument("--min-wait", default="32")
+    ap.add_argument("--min-wait", default="0", help="0: the per-kernel default (comma list)")
     ap.add_argument("--path", default="1")
     ap.add_argument("--far-first", default="0", help="occlusion rays far slots first (comma list)")
     ap.add_argument("--defer", default="1", help="k_path_defer (comma list)")
