@@ -47,3 +47,17 @@ def test_gpus_beyond_visible_devices_fails_loudly():
     r = _run(["--gpus", "2", "--steps", "1"], timeout=120)
     assert r.returncode != 0
     assert "needs 2 visible GPUs" in r.stderr
+
+
+def test_roofline_traffic_from_the_newest_matching_profile():
+    """roofline.traffic is the PMC HBM bytes of the dominant kernel from the newest committed profile
+    of the same workload, looked up under every rocprof name the kernel has had."""
+    c3 = {"triangles": 10_000_002, "width": 1920, "height": 1080, "max_depth": 5, "bvh_leaf": 4, "sah_isect": 4.0,
+          "builder": "sbvh"}
+    t, src = bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, c3, per_spp=1024)
+    newest = sorted((ROOT / "profiles").glob("*_traffic.json"))[-1].name
+    assert src == f"profiles/{newest}" and t is not None and t > 0
+    per_spp = json.loads((ROOT / src).read_text())["kernels"]["k_path<false, true>"]["hbm_bytes_per_spp"]
+    assert t == per_spp * 1024
+    # another workload matches nothing
+    assert bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, dict(c3, triangles=5), per_spp=1) == (None, None)
