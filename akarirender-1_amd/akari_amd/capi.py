@@ -81,10 +81,16 @@ class TraceCounts(C.Structure):
                 ("lane_slots", (C.c_uint64 * 4) * 3), ("deep_rays", C.c_uint64 * 3)]
 
 
+class PixelProbe(C.Structure):
+    _fields_ = [("seed", C.c_uint32), ("closest_rays", C.c_uint32), ("shadow_rays", C.c_uint32), ("flags", C.c_uint32)]
+
+
 TEX_CONSTANT, TEX_IMAGE = 0, 1
 PT_EXACT_CULL = 1
 BUILDER_SAH, BUILDER_LBVH, BUILDER_SBVH = 0, 1, 2
 MAT_DIFFUSE, MAT_GLOSSY, MAT_EMISSIVE, MAT_MIX = 0, 1, 2, 3
+PROBE_SEED, PROBE_RAYS = 1, 2
+FORM_NAMES = {-1: None, 0: "wavefront", 1: "wavefront+lookahead", 2: "k_path", 3: "k_path_defer"}
 
 # numpy views of the POD structs (for vectorised ray/hit buffers)
 RAY_DTYPE = np.dtype([("o", np.float32, 3), ("tmin", np.float32), ("d", np.float32, 3), ("tmax", np.float32)])
@@ -96,6 +102,8 @@ TRI_DTYPE = np.dtype([("v0", np.float32, 3), ("gid", np.uint32), ("e1", np.float
                       ("e2", np.float32, 3), ("_p1", np.uint32)])
 NODE4_DTYPE = np.dtype([("origin", np.float32, 3), ("meta", np.uint32), ("child", np.uint32, 4),
                         ("q", np.uint32, 6), ("_pad", np.uint32, 2)])
+PROBE_DTYPE = np.dtype([("seed", np.uint32), ("closest_rays", np.uint32), ("shadow_rays", np.uint32),
+                        ("flags", np.uint32)])
 LEAF_DTYPE = np.dtype([("lo", np.float32, 3), ("hi", np.float32, 3), ("first", np.uint32), ("count", np.uint32)])
 assert RAY_DTYPE.itemsize == 32 and HIT_DTYPE.itemsize == 32
 assert NODE_DTYPE.itemsize == 64 and TRI_DTYPE.itemsize == 48
@@ -133,6 +141,8 @@ EXPORTS = {
     "akr_hip_reset_stats": (C.c_int, [_P]),
     "akr_hip_render_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "akr_hip_synchronize": (C.c_int, [_P]),
+    "akr_hip_render_form": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "akr_hip_pixel_probe": (C.c_int, [_P, _P, C.c_uint64]),
     "akr_bvh_host_build": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.POINTER(BuildParams), C.POINTER(_P),
                                      C.POINTER(AccelInfo)]),
     "akr_bvh_host_nodes": (_P, [_P]),
@@ -399,6 +409,13 @@ class HipContext:
         self._check(self.lib.akr_hip_render_info(self.h, C.byref(lanes), C.byref(passes)))
         return {"lanes": lanes.value, "passes": passes.value}
 
+    def render_form(self) -> dict:
+        """The form that ran the last path render (FORM_NAMES) and whether its pixel fetch was
+        cost-ordered."""
+        f, o = C.c_int32(0), C.c_int32(0)
+        self._check(self.lib.akr_hip_render_form(self.h, C.byref(f), C.byref(o)))
+        return {"form": FORM_NAMES.get(f.value, str(f.value)), "ordered": bool(o.value)}
+
     def path_profile(self) -> dict:
         """k_path phase profile of the counted launches since reset_stats (ticks: 100 MHz)."""
         out = (C.c_uint64 * 11)()
@@ -416,6 +433,13 @@ class HipContext:
                        slots_tri=c.lane_slots[k][2], visits=c.lane_slots[k][3], deep_rays=c.deep_rays[k])
                for k, m in enumerate(modes)}
         return dict(rays=c.rays, box_tests=c.box_tests, tri_tests=c.tri_tests, per_mode=per)
+
+    def pixel_probe(self, n: int) -> np.ndarray:
+        """Test-only per-slot fingerprint of the last render (option "pixel_probe"): PROBE_DTYPE[n]
+        in packed tile order (final sampler state, closest-hit and shadow traces)."""
+        out = np.zeros(n, PROBE_DTYPE)
+        self._check(self.lib.akr_hip_pixel_probe(self.h, _ptr(out), n))
+        return out
 
     def reset_stats(self):
         self._check(self.lib.akr_hip_reset_stats(self.h))

@@ -176,6 +176,7 @@ struct ShadeArgs {
     uint32_t *shadow_count;
     uint32_t *seed;                // per slot: written when the path ends this bounce
     float4 *L;
+    uint4 *probe;                  // optional, per slot (akr_pixel_probe): .y closest-hit / .z shadow rays
     int32_t depth;
     int32_t max_depth;
     int32_t last;                  // no extension ray is traced after this bounce
@@ -249,6 +250,7 @@ struct RaygenArgs {
     uint32_t *slot_out;
     uint32_t *count_out;
     int32_t first_pass;
+    uint4 *probe;                  // optional, per slot (akr_pixel_probe): .y counts the camera ray
     uint32_t lookahead;            // nonzero: k_raygen_lanes over the planned lanes of `look`
     LookArgs look;
 };
@@ -291,6 +293,9 @@ struct PathArgs {
                                    // shadow result (parity * 8 + bounce), then the waiting extension ray
     uint32_t mix;                  // k_path_defer: scrambled pixel order within each XCD shard
     const uint32_t *order;         // optional: fetch index -> slot (cost-ordered fetch)
+    uint4 *probe;                  // optional, per slot (akr_pixel_probe): final sampler state; the counting
+                                   // build adds the pixel's closest-hit and shadow rays
+    uint32_t *fault;               // mapped host word: set when a wave stops on the hang guard (k_path_defer)
 };
 
 }  // namespace akr

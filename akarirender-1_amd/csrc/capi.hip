@@ -161,6 +161,14 @@ struct akr_hip_ctx {
     bool verify = true;
     DBuf<uint32_t> d_bad;
     uint32_t *h_check = nullptr, *d_check_host = nullptr;
+    // Fault word (mapped, coherent host memory): a persistent kernel's hang guard sets it
+    // (k_path_defer).  Checked after every render on the host, whatever "verify" says.
+    uint32_t *h_fault = nullptr, *d_fault_host = nullptr;
+    // Test-only per-slot fingerprint of the last render (option "pixel_probe", akr_pixel_probe)
+    bool probe = false;
+    DBuf<uint4> d_probe;
+    uint64_t probe_n = 0;
+    bool probe_ok = false;
 
     // host staging (flattened over meshes)
     std::vector<float> verts;
@@ -223,6 +231,7 @@ struct akr_hip_ctx {
     bool cur_look = false;
     bool la_early_exit = true;            // diagnostic: false runs all spp passes
     int last_lanes = 1, last_passes = 0;
+    int32_t last_form = AKR_FORM_NONE, last_ordered = 0;  // akr_hip_render_form
     // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
     // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
     // Both internal: `main` (high priority) runs raygen / closest-hit / shade, `side` (low priority)
@@ -315,6 +324,7 @@ struct akr_hip_ctx {
             if (e) (void)hipEventDestroy(e);
         if (h_remain) (void)hipHostFree(h_remain);
         if (h_check) (void)hipHostFree(h_check);
+        if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (main_st) (void)hipStreamDestroy(main_st);
         if (side) (void)hipStreamDestroy(side);
@@ -548,6 +558,22 @@ struct akr_hip_ctx {
         HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_remain), 2 * sizeof(uint32_t),
                              hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_remain_host), h_remain, 0));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_fault), sizeof(uint32_t),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_fault_host), h_fault, 0));
+        *reinterpret_cast<volatile uint32_t *>(h_fault) = 0;
+    }
+
+    // A raised fault word fails the call that sees it (and is cleared): the hang guard of a
+    // persistent kernel stopped a wave, so that render's film is incomplete.  Called after the host
+    // has waited for a render; a render_device without "verify" reports it at the next call.
+    void check_fault() {
+        if (!h_fault) return;
+        volatile uint32_t *f = reinterpret_cast<volatile uint32_t *>(h_fault);
+        if (*f == 0) return;
+        *f = 0;
+        throw std::runtime_error("persistent path kernel: a wave stopped on its hang guard; the film of the render "
+                                 "that raised it is incomplete");
     }
 
     uint32_t grid_for(int mode, uint64_t n) const {
@@ -734,6 +760,7 @@ struct akr_hip_ctx {
         launch_store_word(d_bad.p, d_check_host, st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(st));
+        check_fault();
         const uint32_t bad = read_mapped(h_check);
         if (bad == kMappedSentinel) throw std::runtime_error("film check: the device never reported its result");
         if (bad != 0)
@@ -786,10 +813,23 @@ struct akr_hip_ctx {
         const size_t n_count_words = 2 * (size_t)D * kWorkStride + 2 * (size_t)D * kTraceWords;
         last_lanes = 1;
         last_passes = 0;
+        last_form = AKR_FORM_NONE;
+        last_ordered = 0;
         // lookahead needs every sample length in the histogram's range: max_depth <= 10
         const bool look_ok = p.spp >= 2 && 3u * (uint32_t)p.max_depth + 1u <= kLookBins;
+        probe_ok = false;
+        probe_n = 0;
         const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st, look_ok);
         if (N == 0) return 0;
+        check_fault();  // a fault raised by an earlier render_device that ran without "verify"
+        uint4 *probe_p = nullptr;  // option "pixel_probe" (not with lookahead lanes)
+        if (probe && !cur_look) {
+            d_probe.reserve(N);
+            HIPCHK(hipMemsetAsync(d_probe.p, 0, N * sizeof(uint4), main_st));
+            probe_p = d_probe.p;
+            probe_n = N;
+            probe_ok = true;
+        }
         // Lookahead: lanes of a pixel run the samples that start at planned draw
         // offsets from its committed sampler state; k_la_accept keeps the chain of lanes that start
         // at real sample boundaries.  Slot j = lane * R + r over the pass's R active pixels.
@@ -863,6 +903,8 @@ struct akr_hip_ctx {
                 pa.max_depth = p.max_depth;
                 pa.ray_clamp = p.ray_clamp;
                 pa.prof = count ? d_pprof.p : nullptr;
+                pa.probe = probe_p;
+                pa.fault = d_fault_host;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
                 // the shading's material / light / CDF tables in LDS when they fit
@@ -888,11 +930,14 @@ struct akr_hip_ctx {
                 }
                 timed("path", ms, [&] { launch_path(count, defer, tab, pa, grid, ms); });
                 HIPCHK(hipGetLastError());
+                last_form = defer ? AKR_FORM_PATH_DEFER : AKR_FORM_PATH;
+                last_ordered = pa.order ? 1 : 0;
             }
             last_passes = 1;
             join_streams(st);
             return N;
         }
+        if (p.spp > 0) last_form = la ? AKR_FORM_LOOKAHEAD : AKR_FORM_WAVEFRONT;
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
         int64_t g = 0;  // bounce index over all passes: shadow queues alternate by its parity
@@ -916,6 +961,7 @@ struct akr_hip_ctx {
             if (s >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ps], 0));
             HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
             RaygenArgs rg = raygen_args(la ? (uint32_t)S : (uint32_t)N, L, qcount(0), s == 0);
+            rg.probe = probe_p;
             if (la) {
                 rg.lookahead = 1;
                 rg.look = look(ps);
@@ -950,6 +996,7 @@ struct akr_hip_ctx {
                 sh.depth = b;
                 sh.max_depth = p.max_depth;
                 sh.last = b == nb - 1;
+                sh.probe = probe_p;
                 timed("shade", ms, [&] { launch_shade(sh, (uint32_t)S, ms); });
                 HIPCHK(hipEventRecord(ev_shade[sq], ms));
                 HIPCHK(hipStreamWaitEvent(side, ev_shade[sq], 0));
@@ -997,6 +1044,8 @@ struct akr_hip_ctx {
             timed("splat", side, [&] { launch_splat(sp, (uint32_t)N, side); });
             HIPCHK(hipEventRecord(ev_splat[ps], side));
         }
+        // the last shade of every pass ran on the main stream and left each slot's sampler state
+        if (probe_p && p.spp > 0) launch_probe_seed(d_seed.p, (uint32_t)N, probe_p, ms);
         join_streams(st);
         return N;
     }
@@ -1012,6 +1061,8 @@ struct akr_hip_ctx {
         if (p.spp < 0) throw std::runtime_error("spp must be >= 0");
         // per pass: camera-queue count, AO-queue count, then 2 trace launches x kTraceWords
         const size_t n_count_words = 2 * (size_t)kWorkStride + 2 * (size_t)kTraceWords;
+        probe_ok = false;
+        probe_n = 0;
         const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st);
         if (N == 0) return 0;
         const bool shadow_mode = std::isinf(p.occlude) && p.occlude > 0;
@@ -1193,6 +1244,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_min_wait") {
             if (value < 0 || value > 64) throw std::runtime_error("path_min_wait must be in [0, 64] (0: per kernel)");
             ctx->path_min_wait = (int)value;
+        } else if (k == "pixel_probe") {
+            ctx->probe = value != 0;
         } else if (k == "verify") {
             ctx->verify = value != 0;
         } else if (k == "la_early_exit") {
@@ -1426,6 +1479,11 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
             hipStream_t st = c->stream;
             const uint64_t N = c->render(*params, part[k].data(), (int32_t)part[k].size(), st);
             c->verify_weights(st, N, params->spp);  // joins the render into st and checks it
+            if (!c->verify) {
+                c->join_streams(st);
+                HIPCHK(hipStreamSynchronize(st));
+                c->check_fault();
+            }
             c->mark_done(st);
             npix[k] = N;
         });
@@ -1510,6 +1568,7 @@ void merge_film(akr_hip_ctx *ctx, uint64_t N, int spp, float *radiance, float *w
     // cross-stream event waits (two flaky short-weight reads were seen, never reproduced)
     ctx->host_join();
     HIPCHK(hipStreamSynchronize(st));
+    ctx->check_fault();
     ctx->verify_weights(st, N, spp);
     std::vector<float4> film(N);
     HIPCHK(hipMemcpyAsync(film.data(), ctx->d_film.p, N * sizeof(float4), hipMemcpyDeviceToHost, st));
@@ -1696,6 +1755,13 @@ int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes) {
     });
 }
 
+int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered) {
+    return guard(ctx, [&] {
+        if (form) *form = ctx->last_form;
+        if (ordered) *ordered = ctx->last_ordered;
+    });
+}
+
 int akr_hip_reset_stats(akr_hip_ctx *ctx) {
     return guard(ctx, [&] {
         HIPCHK(hipDeviceSynchronize());
@@ -1710,6 +1776,21 @@ int akr_hip_synchronize(akr_hip_ctx *ctx) {
     return guard(ctx, [&] {
         HIPCHK(hipStreamSynchronize(ctx->stream));
         HIPCHK(hipDeviceSynchronize());
+        ctx->check_fault();
+    });
+}
+
+int akr_hip_pixel_probe(akr_hip_ctx *ctx, akr_pixel_probe *out, uint64_t n) {
+    return guard(ctx, [&] {
+        if (!ctx->probe_ok || n > ctx->probe_n)
+            throw std::runtime_error("no pixel probe recorded for that many slots (option pixel_probe, path renders only)");
+        if (n == 0) return;
+        if (!out) throw std::runtime_error("null output");
+        static_assert(sizeof(akr_pixel_probe) == sizeof(uint4), "akr_pixel_probe layout");
+        ctx->host_join();
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipMemcpyAsync(out, ctx->d_probe.p, n * sizeof(uint4), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
     });
 }
 

@@ -793,6 +793,7 @@ __global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
     a.ray_out[2 * (size_t)i + 1] = r1;
     a.state_out[i] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
     a.slot_out[i] = i;
+    if (a.probe) a.probe[i].y += 1u;  // the camera ray (always traced)
     if (i == 0) *a.count_out = a.n;
 }
 
@@ -1290,6 +1291,12 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(ShadeArgs a) {
         // the path does not reach another traced bounce: persist its sampler stream for the next
         // sample pass (the stream continues across spp, cpu/integrator.cpp:124-134)
         if (!bo.ext) a.seed[slot] = seed;
+        if (a.probe && (bo.ext || bo.sh)) {  // one queue entry per slot per launch: no race
+            uint4 q = a.probe[slot];
+            q.y += bo.ext ? 1u : 0u;
+            q.z += bo.sh ? 1u : 0u;
+            a.probe[slot] = q;
+        }
     }
     uint32_t pos, spos;
     block_append2<kShadeBlock>(bo.ext, a.count_out, pos, bo.sh, a.shadow_count, spos);
@@ -1674,6 +1681,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     bool pend = false;
     bool any = false;           // the lane's ray is a shadow ray (a hit is bgid != kNoHit)
     bool need_pixel = true, done = false, fin = false, busy = false;
+    uint32_t pc_closest = 0, pc_shadow = 0;  // counting build: the pixel's rays (akr_pixel_probe)
     PathRay r{};
     r.best = kInf;
     r.bgid = kNoHit;
@@ -1770,6 +1778,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 splat_one(film, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
                 if (--left == 0) {
                     pa.film[pix] = film;
+                    if (pa.probe)
+                        pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
+                                                   COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
                     need_pixel = true;
                 } else {
                     start = true;
@@ -1784,6 +1795,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
                 film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 start = true;
+                if (COUNT) pc_closest = pc_shadow = 0;
             }
             if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
                 Lr = V3{0.0f, 0.0f, 0.0f};
@@ -1797,6 +1809,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             path_unpark(s_park, tid, r, ff, any);  // the busy lanes' traversal continues unchanged
             if (fresh) {
                 any = next_any;
+                if (COUNT) {
+                    pc_closest += any ? 0u : 1u;
+                    pc_shadow += any ? 1u : 0u;
+                }
                 busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
                 fin = !busy;
             }
@@ -1925,6 +1941,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     DeferState s;
     bool need_pixel = true, done = false, fin = false, busy = false;
     uint32_t idle_rounds = 0;    // hang guard: consecutive rounds with no ray in flight in the wave
+    uint32_t pc_closest = 0, pc_shadow = 0;  // counting build: the owned pixel's rays (akr_pixel_probe)
     PathRay r{};
     r.best = kInf;
     r.bgid = kNoHit;
@@ -2011,6 +2028,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                             s.set(DeferState::DEPTH, 4, (uint32_t)depth + 1u);
                         }
                         if (bo.sh) {
+                            if (COUNT) pc_shadow++;  // the owner's pixel, whichever lane traces it
                             const uint32_t rp = s.rp(), b = s.nsh(rp), slot = rp * kDeferSlots + b;
                             s.set(DeferState::NSH + 4 * rp, 4, b + 1u);
                             contrib[slot * lanes] = make_float4(bo.col.x, bo.col.y, bo.col.z, 0.0f);
@@ -2071,6 +2089,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             const bool free_lane = !busy && !fresh && !want_sh && s.kind() == RAY_NONE;
             if (free_lane && !done && !need_pixel && !s.running() && left == 0 && s.open() == 0) {
                 pa.film[pix] = film;
+                if (pa.probe)
+                    pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
+                                               COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
                 need_pixel = true;
             }
             const bool asked = need_pixel && !done;
@@ -2080,6 +2101,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 left = pa.spp;
                 seed = (uint32_t)((int)(pxy & 0xFFFFu) + (int)(pxy >> 16) * pa.cam.width);
                 film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (COUNT) pc_closest = pc_shadow = 0;
             }
             try_start(free_lane, fresh, ra, rb);
             // 5. hand the new shadow rays to the wave's lanes that have nothing in hand, in lane order
@@ -2139,6 +2161,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             const uint32_t kind_now = s.kind();
             path_unpark(s_park, tid, r, ff, kind_now == RAY_OWN_SHADOW || kind_now == RAY_FOREIGN);
             if (fresh) {
+                if (COUNT) pc_closest += occl ? 0u : 1u;  // own extension / camera rays
                 busy = path_begin<COUNT>(a, occl, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
                 fin = !busy;
             }
@@ -2150,9 +2173,12 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         }
         if (!__any(busy)) {
             // nothing in flight: every result is posted, so the next round makes progress; a wave
-            // that idles for many rounds has lost its state (a bug): stop instead of spinning (the
-            // render's in-band weight check then reports it)
-            if (++idle_rounds > 1024) break;
+            // that idles for many rounds has lost its state (a bug): stop instead of spinning, and
+            // raise the fault word the host checks after every render (akr_hip_ctx::check_fault)
+            if (++idle_rounds > 1024) {
+                if (pa.fault && __lane_id() == 0) __hip_atomic_fetch_or(pa.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
             continue;
         }
         idle_rounds = 0;
@@ -2241,6 +2267,17 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, ui
 }
 
 // one word from device memory into mapped host memory (the host polls it after an event)
+// Wavefront form: the final sampler state of every slot into its pixel probe (the ray counts were
+// added by k_raygen / k_shade)
+__global__ __launch_bounds__(kBlock) void k_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint4 q = probe[i];
+    q.x = seed[i];
+    q.w = AKR_PROBE_SEED | AKR_PROBE_RAYS;
+    probe[i] = q;
+}
+
 __global__ void k_store_word(const uint32_t *src, uint32_t *dst) {
     if (threadIdx.x == 0) {
         __atomic_store_n(dst, *src, __ATOMIC_RELAXED);
@@ -2371,6 +2408,10 @@ void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, 
 void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t *key, uint32_t *idx, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift, key, idx);
+}
+void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_probe_seed, dim3(blocks_for(n)), dim3(kBlock), 0, st, seed, n, probe);
 }
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
     if (n == 0) return;

@@ -1,5 +1,8 @@
-"""Headline benchmark: Msamples/s of the wavefront path tracer on the synthetic 10M-triangle soup
+"""Headline benchmark: Msamples/s of the HIP path tracer on the synthetic 10M-triangle soup
 (BASELINE.json configs[2] / SURVEY.md §8d C3), 1920x1080, max_depth 5, tile-split across ranks.
+The render form is the library's choice (the persistent path kernel on this scene);
+config.form names it, and an untimed same-run leg reports north_star's wavefront layout beside it
+(wavefront_ms_per_step).
 
 A step is one sample per pixel over the whole frame (2,073,600 path samples).  K steps are one
 render(spp=K) call per rank over that rank's tiles; the frame-end gather to rank 0 (RCCL via
@@ -121,13 +124,41 @@ def launch_plan(gpus: int, env) -> tuple:
     return ("rank", world)
 
 
+KFD_NODES = Path("/sys/class/kfd/kfd/topology/nodes")
+
+
+def visible_gpu_count(env=None, kfd_nodes: Path = KFD_NODES) -> int:
+    """GPUs this process may use, counted without torch or the HIP runtime (the launcher must not
+    initialise the GPU before it starts the ranks: torch.cuda.device_count() can fall back to
+    hipGetDeviceCount on this image).  KFD topology nodes with a non-zero gpu_id are the GPU agents;
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES narrow them as the runtime would.
+    Each rank still checks its own device when it starts."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        for node in kfd_nodes.iterdir():
+            try:
+                if int((node / "gpu_id").read_text().strip() or "0") != 0:
+                    n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids))
+    return n
+
+
 def spawn_ranks(n: int, argv, need_devices: bool = True) -> int:
     """Start n ranks of this script as a torch.distributed.run child (one process per GPU, RCCL
-    over 127.0.0.1 rendezvous) and return its exit code.  Only counts devices first
-    (torch.cuda.device_count does not initialise the GPU), so no HIP state exists in this process."""
+    over 127.0.0.1 rendezvous) and return its exit code.  Counts devices from sysfs first
+    (visible_gpu_count): neither torch.cuda nor the HIP runtime is touched in this process, so the
+    child start is never an exec after GPU initialisation."""
     if need_devices:
-        import torch
-        have = torch.cuda.device_count()
+        have = visible_gpu_count()
         if have < n:
             raise SystemExit(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -204,6 +235,8 @@ def main():
     ap.add_argument("--slot-target", type=int, default=0, help="auto lookahead: path slots per render (0: library default)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
+    ap.add_argument("--wavefront-spp", type=int, default=8,
+                    help="untimed same-run leg in the wavefront form (north_star's layout), spp; 0 = skip")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -221,6 +254,8 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
+        if torch.cuda.device_count() <= local:
+            raise SystemExit(f"bench.py: rank {rank} needs device {local}, {torch.cuda.device_count()} visible")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         live = dist.get_world_size()   # n_gpus is the live group's size, never a flag
@@ -309,6 +344,7 @@ def main():
         dist.all_gather_into_tensor(gathered, film)     # frame-end gather over RCCL
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    form = ctx.render_form()   # which form the library ran
     if world > 1:
         dist.barrier()
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -334,6 +370,23 @@ def main():
         torch.cuda.synchronize(dev)
         iso = ctx.kernel_stats()
         ctx.set_option("serial_shadow", 0)
+    # untimed same-run leg in north_star's layout (wavefront: raygen -> closest -> shade -> shadow
+    # -> splat launches per bounce), when the timed render ran a persistent kernel
+    wavefront = None
+    if rank == 0 and args.wavefront_spp > 0 and form["form"] in ("k_path", "k_path_defer"):
+        ctx.reset_stats()
+        ctx.set_option("stats", 0)
+        ctx.set_option("path", 0)
+        ctx.render_device(1, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)   # warm
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
+        ctx.render_device(args.wavefront_spp, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter() - tw
+        assert ctx.render_form()["form"] == "wavefront"
+        ctx.set_option("path", args.path)
+        wavefront = {"ms_per_step": round(tw / args.wavefront_spp * 1e3, 3), "spp": args.wavefront_spp,
+                     "Msamples_per_s": round(npix * args.wavefront_spp / tw / 1e6, 3), "timed": False}
 
     if rank != 0:
         if world > 1:
@@ -345,6 +398,7 @@ def main():
                           "rank_ms_per_step": round(elapsed / K * 1e3, 3),
                           "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3), "lookahead": la,
                           "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3),
+                          "form": form, "wavefront": wavefront,
                           "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                                       for k, v in bstats.items()},
                           "rays_per_pixel": {"closest": counts["per_mode"]["closest"]["rays"] / max(1, npix),
@@ -371,8 +425,13 @@ def main():
     traffic, traffic_src = measured_traffic(prof_name, {
         "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf,
         "sah_isect": args.sah_isect, "builder": args.builder}, per_spp=K if dom == "path" else None)
+    # hardware fraction beside the model one: the PMC-measured HBM bytes of the same kernel (committed
+    # profile of this workload) over the live launch time
+    hbm_achieved = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "hbm_achieved": round(hbm_achieved, 1) if hbm_achieved else None,
+                "hbm_frac": round(hbm_achieved / HBM_PEAK_GBS, 4) if hbm_achieved else None,
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
                 "kernel": dom, "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
                 "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
@@ -436,7 +495,12 @@ def main():
                                         "area lights (scene.hall_scene)"}[args.scene], "triangles": cs.n_tris,
                    "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
                    "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
-                   "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la},
+                   "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la,
+                   # the form the library ran (north_star names a wavefront; DESIGN.md §0 / §3.8 give the
+                   # measured reason for the persistent kernel on this scene) and the wavefront beside it
+                   "form": form["form"], "ordered_fetch": form["ordered"]},
+        "wavefront_ms_per_step": wavefront["ms_per_step"] if wavefront else None,
+        "wavefront": wavefront,
         "roofline": roofline, "cpu_baseline": cpu,
         # per-kernel averages from an untimed pass with events on every launch (the timed region
         # times trace_closest only: events around every launch cost ~7 % at an 8-way rank)

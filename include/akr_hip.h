@@ -46,7 +46,8 @@
 extern "C" {
 #endif
 
-#define AKR_HIP_API_VERSION 1
+/* 2: akr_trace_counts gained deep_rays[3]; akr_pixel_probe / akr_hip_pixel_probe added */
+#define AKR_HIP_API_VERSION 2
 
 typedef struct akr_hip_ctx akr_hip_ctx;
 
@@ -178,6 +179,21 @@ typedef struct akr_trace_counts {
     uint64_t deep_rays[3];
 } akr_trace_counts;
 
+/* Test-only per-pixel fingerprint of the last render's sample loop (option "pixel_probe" = 1),
+ * one record per film slot in packed tile order (as akr_hip_render_device): the LCG state after the
+ * pixel's last sample (its draw count encodes every path length, kernel/sampler.h:54-67), and the
+ * closest-hit and shadow traces of all its samples (pathtracer.h:69-91, 133-164).  The seed is
+ * recorded by every render form; the ray counts by the wavefront form and by the counting build of
+ * the persistent kernels (option "count_tests"), flagged in `flags`. */
+#define AKR_PROBE_SEED 1u
+#define AKR_PROBE_RAYS 2u
+typedef struct akr_pixel_probe {
+    uint32_t seed;
+    uint32_t closest_rays;   /* camera + extension rays traced (none at depth == max_depth) */
+    uint32_t shadow_rays;    /* NEE shadow rays traced */
+    uint32_t flags;          /* AKR_PROBE_SEED | AKR_PROBE_RAYS: which fields were recorded */
+} akr_pixel_probe;
+
 int akr_hip_api_version(void);
 int akr_hip_device_count(int *n);
 
@@ -269,7 +285,20 @@ int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
 /* The last akr_hip_render's lookahead lanes per pixel and sample passes launched (diagnostic). */
 int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
+/* Which form ran the last path render (all give the same bits): the wavefront
+ * kernels (north_star's layout: raygen -> closest -> shade -> shadow -> splat launches), lookahead
+ * lanes over the wavefront, the persistent path kernel, or its deferred-NEE form; *ordered = 1 when
+ * the persistent kernel fetched pixels in pilot-cost order.  AKR_FORM_NONE: nothing rendered. */
+#define AKR_FORM_NONE (-1)
+#define AKR_FORM_WAVEFRONT 0
+#define AKR_FORM_LOOKAHEAD 1
+#define AKR_FORM_PATH 2
+#define AKR_FORM_PATH_DEFER 3
+int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered);
 int akr_hip_synchronize(akr_hip_ctx *ctx);
+/* Copies the first n records of the last render's pixel probe (see akr_pixel_probe); fails when
+ * the last render ran without option "pixel_probe" or has fewer slots. */
+int akr_hip_pixel_probe(akr_hip_ctx *ctx, akr_pixel_probe *out, uint64_t n);
 /* Diagnostic: with option "ray_steps" set, each standalone trace (akr_hip_trace /
  * akr_hip_trace_device) runs the counting kernel and records, per ray, the traversal-loop
  * iterations it was active for plus its triangle tests (0xFFFFFFFF: traced by the exact BVH2

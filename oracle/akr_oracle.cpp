@@ -512,12 +512,19 @@ inline bool is_black(V3 c) {
 
 struct PathStats { uint64_t cam = 0, ext = 0, shd = 0, box = 0, tri = 0; };
 
+// Per-pixel fingerprint of the sample loop (akr_pixel_probe): closest-hit traces the device makes
+// (every trace below max(1, max_depth): the one at depth == max_depth can add nothing and the
+// device skips it) and shadow traces; the final sampler state is taken by the caller.
+struct PixelTally { uint32_t closest = 0, shadow = 0; };
+
 // GenericPathTracer::run_megakernel (pathtracer.h:133-164) with on_surface_scatter (:96-132)
 // and compute_direct_lighting (:69-91); returns L.
-V3 trace_path(const Scene &sc, Lcg &sampler, int x, int y, int max_depth, bool tight, PathStats &st) {
+V3 trace_path(const Scene &sc, Lcg &sampler, int x, int y, int max_depth, bool tight, PathStats &st,
+               PixelTally &pt) {
     const orc_scene &s = *sc.s;
     V3 L = v3(0, 0, 0), beta = v3(1, 1, 1);
     int depth = 0;
+    const int traced_below = max_depth == 0 ? 1 : max_depth;
     V2 u1 = sampler.next2d();  // lens sample (unused: lens_radius = 0)
     (void)u1;
     V2 u2 = sampler.next2d();
@@ -526,6 +533,7 @@ V3 trace_path(const Scene &sc, Lcg &sampler, int x, int y, int max_depth, bool t
     st.cam++;
     while (true) {
         Best hit;
+        if (depth < traced_below) pt.closest++;
         if (!traverse(s, ray, false, tight, hit, st.box, st.tri)) break;
         V3 wo = neg(ray.d);
         Tri tri = get_triangle(s, hit.gid);
@@ -616,6 +624,7 @@ V3 trace_path(const Scene &sc, Lcg &sampler, int x, int y, int max_depth, bool t
                 V3 color = divs(mul(beta, fl), light_pdf);
                 if (!is_black(color)) {
                     st.shd++;
+                    pt.shadow++;
                     Best sh;
                     if (!traverse(s, shadow, true, tight, sh, st.box, st.tri)) L = add(L, color);
                 }
@@ -814,8 +823,9 @@ int orc_trace_brute(const orc_scene *s, const akr_ray *rays, uint64_t n, orc_hit
     return 0;
 }
 
-int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles, int32_t n_tiles, float *radiance,
-               float *weight, int32_t n_threads, orc_render_stats *stats) {
+int orc_render_probe(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles, int32_t n_tiles,
+                     float *radiance, float *weight, int32_t n_threads, orc_render_stats *stats,
+                     akr_pixel_probe *probe) {
     Scene sc;
     sc.s = s;
     sc.cam = make_camera(s->camera);
@@ -837,8 +847,9 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
                 Lcg sampler{(uint32_t)(x + y * W)};  // set_sample_index(x + y * W), integrator.cpp:124
                 V3 acc = v3(0, 0, 0);
                 float wsum = 0;
+                PixelTally pt;
                 for (int sidx = 0; sidx < p->spp; sidx++) {
-                    V3 L = trace_path(sc, sampler, x, y, p->max_depth, tight, pst[tid]);
+                    V3 L = trace_path(sc, sampler, x, y, p->max_depth, tight, pst[tid], pt);
                     if (clampv > 0) {  // gpu/cuda/integrator.cpp:397-398 (GPU-only clamp)
                         V3 c;
                         c.x = std::isnan(L.x) ? 0.0f : rmax(0.0f, L.x);
@@ -854,6 +865,13 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
                 o[1] = acc.y;
                 o[2] = acc.z;
                 o[3] = wsum;
+                if (probe) {  // frame-indexed; a pixel listed twice computes the same values
+                    akr_pixel_probe &q = probe[(size_t)x + (size_t)y * (size_t)W];
+                    q.seed = sampler.seed;
+                    q.closest_rays = pt.closest;
+                    q.shadow_rays = pt.shadow;
+                    q.flags = AKR_PROBE_SEED | AKR_PROBE_RAYS;
+                }
             }
     });
     tf.merge(work, W, radiance, weight);
@@ -868,6 +886,11 @@ int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles
         }
     }
     return 0;
+}
+
+int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles, int32_t n_tiles, float *radiance,
+               float *weight, int32_t n_threads, orc_render_stats *stats) {
+    return orc_render_probe(s, p, tiles, n_tiles, radiance, weight, n_threads, stats, nullptr);
 }
 
 int orc_render_ao(const orc_scene *s, const akr_ao_params *p, const akr_rect *tiles, int32_t n_tiles, float *radiance,

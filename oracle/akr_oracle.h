@@ -94,6 +94,14 @@ int orc_trace_brute(const orc_scene *s, const akr_ray *rays, uint64_t n, orc_hit
  * (core/parallel.cpp:44-129); accumulates into full-frame radiance[W*H*3], weight[W*H]. */
 int orc_render(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles, int32_t n_tiles,
                float *radiance, float *weight, int32_t n_threads, orc_render_stats *stats);
+/* orc_render plus a per-pixel fingerprint of the sample loop into the frame-indexed probe[W*H]
+ * (pixels outside the tiles untouched): the sampler state after the pixel's last sample (its draw
+ * count encodes every path length and BSDF-pdf rejection), the closest-hit traces below
+ * max(1, max_depth) and the shadow traces, summed over the pixel's samples
+ * (pathtracer.h:69-91, 133-164; cpu/integrator.cpp:124-134). */
+int orc_render_probe(const orc_scene *s, const akr_pt_params *p, const akr_rect *tiles, int32_t n_tiles,
+                     float *radiance, float *weight, int32_t n_threads, orc_render_stats *stats,
+                     akr_pixel_probe *probe);
 /* cpu::AmbientOcclusion::render (kernel/integrators/cpu/integrator.cpp:40-87) over the pixels of
  * `tiles`, same work split; L is 1 when the cosine-sampled ray from the camera hit (frame of the
  * geometric normal, tmin Eps) has no closest hit with t < occlude, 0 otherwise or on a camera miss.

@@ -66,6 +66,8 @@ def lib():
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.orc_trace_brute.argtypes = [C.POINTER(OrcScene), _P, C.c_uint64, _P, C.c_int, C.c_int32]
         l.orc_render.argtypes = [C.POINTER(OrcScene), _P, _P, C.c_int32, _P, _P, C.c_int32, C.POINTER(OrcStats)]
+        l.orc_render_probe.argtypes = [C.POINTER(OrcScene), _P, _P, C.c_int32, _P, _P, C.c_int32,
+                                       C.POINTER(OrcStats), _P]
         l.orc_render_ao.argtypes = [C.POINTER(OrcScene), _P, _P, C.c_int32, _P, _P, C.c_int32, C.POINTER(OrcStats)]
         _lib = l
     return _lib
@@ -166,6 +168,7 @@ class OracleScene:
         pw = arr(cs.power, np.float32)
         nd = arr(nodes, nodes.dtype)
         tr = arr(tris, tris.dtype)
+        self.nodes, self.tris = nd, tr  # shareable with another camera's OracleScene
         s = OrcScene()
         s.vertices, s.n_vertices = _p(v), v.shape[0]
         s.indices, s.normals, s.texcoords, s.matid, s.n_tris = _p(i), _p(n), _p(t), _p(m), m.shape[0]
@@ -196,7 +199,9 @@ class OracleScene:
         return hits
 
     def render(self, spp, max_depth, tiles=None, ray_clamp=0.0, n_threads=0, radiance=None, weight=None,
-               exact_cull=False):
+               exact_cull=False, probe=False):
+        """cpu::PathTracer::render restated; with probe=True also returns the frame-indexed per-pixel
+        fingerprint (capi.PROBE_DTYPE [H, W]: final sampler state, closest-hit / shadow traces)."""
         W, H = self.width, self.height
         if tiles is None:
             tiles = [(0, 0, W, H)]
@@ -207,10 +212,13 @@ class OracleScene:
         p = self.capi.PtParams(int(spp), int(max_depth), float(ray_clamp), 1 if exact_cull else 0)
         rects = (self.capi.Rect * max(1, len(tiles)))(*[self.capi.Rect(*t) for t in tiles])
         st = OrcStats()
-        lib().orc_render(C.byref(self.s), C.byref(p), C.cast(rects, _P), len(tiles), _p(radiance), _p(weight),
-                         n_threads, C.byref(st))
+        pr = np.zeros((H, W), self.capi.PROBE_DTYPE) if probe else None
+        lib().orc_render_probe(C.byref(self.s), C.byref(p), C.cast(rects, _P), len(tiles), _p(radiance), _p(weight),
+                               n_threads, C.byref(st), _p(pr))
         stats = dict(camera_rays=st.camera_rays, extension_rays=st.extension_rays, shadow_rays=st.shadow_rays,
                      box_tests=st.box_tests, tri_tests=st.tri_tests)
+        if probe:
+            return radiance, weight, stats, pr
         return radiance, weight, stats
 
     def render_ao(self, spp, tiles=None, occlude=float("inf"), n_threads=0, radiance=None, weight=None,

@@ -185,3 +185,37 @@ def refpng_verdict(z):
     fails = [(int(r), int(c), round(float(z[r, c]), 1)) for r, c in np.argwhere(outside & ~ok)]
     gap_darker = int(np.count_nonzero(gap & (z < -3)))
     return ok[outside].mean(), fails, gap_darker
+
+
+def slot_pixels(tiles, width, height):
+    """(ys, xs) of every film slot in packed tile order (tiles clipped to the frame, row-major
+    inside a tile): the order of akr_hip_render_device's output and of akr_hip_pixel_probe."""
+    ys, xs = [], []
+    for x0, y0, x1, y1 in tiles:
+        x0, y0, x1, y1 = max(0, x0), max(0, y0), min(width, x1), min(height, y1)
+        if x1 <= x0 or y1 <= y0:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1]
+        ys.append(yy.reshape(-1))
+        xs.append(xx.reshape(-1))
+    if not ys:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    return np.concatenate(ys), np.concatenate(xs)
+
+
+def check_probe(gpu, orc_frame, tiles, width, height, what=""):
+    """Compare a device pixel probe (slot order) with the oracle's frame-indexed probe: the final
+    sampler state always, the ray counts when the device recorded them.  Returns whether it
+    compared ray counts."""
+    ys, xs = slot_pixels(tiles, width, height)
+    exp = orc_frame[ys, xs]
+    assert len(gpu) == len(exp)
+    assert np.all(gpu["flags"] & capi.PROBE_SEED), f"{what}: seeds not recorded"
+    bad = np.count_nonzero(gpu["seed"] != exp["seed"])
+    assert bad == 0, f"{what}: {bad} of {len(exp)} final sampler states differ from the oracle"
+    rays = bool(np.all(gpu["flags"] & capi.PROBE_RAYS))
+    if rays:
+        for k in ("closest_rays", "shadow_rays"):
+            bad = np.count_nonzero(gpu[k] != exp[k])
+            assert bad == 0, f"{what}: {bad} of {len(exp)} per-pixel {k} differ from the oracle"
+    return rays

@@ -41,8 +41,7 @@ def test_gpus_2_spawns_two_gloo_ranks():
 
 def test_gpus_beyond_visible_devices_fails_loudly():
     # this container has no GPU: asking for 2 ranks of real work must fail before any rank starts
-    import torch
-    if torch.cuda.device_count() >= 2:
+    if bench.visible_gpu_count() >= 2:
         pytest.skip("two or more devices visible")
     r = _run(["--gpus", "2", "--steps", "1"], timeout=120)
     assert r.returncode != 0
@@ -61,3 +60,38 @@ def test_roofline_traffic_from_the_newest_matching_profile():
     assert t == per_spp * 1024
     # another workload matches nothing
     assert bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, dict(c3, triangles=5), per_spp=1) == (None, None)
+
+
+def test_visible_gpu_count_from_sysfs(tmp_path):
+    """Devices are counted from the KFD topology (gpu_id != 0: CPU nodes have 0), narrowed by the
+    visibility variables, without torch or HIP."""
+    for i, gid in enumerate((0, 4242, 0, 777, 999)):
+        (tmp_path / str(i)).mkdir()
+        (tmp_path / str(i) / "gpu_id").write_text(f"{gid}\n")
+    (tmp_path / "9").mkdir()   # a node without gpu_id is skipped
+    assert bench.visible_gpu_count({}, tmp_path) == 3
+    assert bench.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1"}, tmp_path) == 2
+    assert bench.visible_gpu_count({"ROCR_VISIBLE_DEVICES": ""}, tmp_path) == 0
+    assert bench.visible_gpu_count({}, tmp_path / "missing") == 0
+
+
+def test_spawn_path_never_initialises_the_gpu_in_the_parent():
+    """--gpus N's launcher counts devices and starts the ranks without importing torch.cuda state or
+    loading the HIP runtime into the parent (exec after GPU init takes the machine down on the pool):
+    the parent's memory map holds no libamdhip64 and torch is never imported."""
+    code = f"""
+import sys
+sys.path.insert(0, {str(ROOT)!r})
+import bench
+bench.visible_gpu_count = lambda *a, **k: 2   # the count itself is tested separately
+rc = bench.spawn_ranks(2, ["--launch-check"], need_devices=True)
+maps = open("/proc/self/maps").read()
+assert rc == 0, rc
+assert "libamdhip64" not in maps, "HIP runtime loaded in the launcher"
+assert "torch" not in sys.modules, "torch imported in the launcher"
+print("LAUNCHER-CLEAN")
+"""
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=str(ROOT))
+    assert r.returncode == 0 and "LAUNCHER-CLEAN" in r.stdout, r.stderr[-3000:]

@@ -10,12 +10,14 @@ oracle would take minutes, size-independent properties: every pixel holds exactl
 the frame is the same bit for bit whether rendered whole or as one rank's share of an 8-way split
 (pixels are independent, cpu/integrator.cpp:124).
 """
+import dataclasses
+
 import numpy as np
 import pytest
 
 import py_oracle
 from akari_amd import capi, dist, scene
-from helpers import hits_to_gid, random_rays
+from helpers import check_probe, hits_to_gid, random_rays
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
@@ -115,7 +117,7 @@ def test_c3_render_tile_subset_bit_exact(c3):
     # NEE runs (shadow rays are traced), though the 1-cm mean free path of the soup occludes the
     # emitter above it from everything the camera sees: the C3 frame is dark by construction
     assert st["shadow_rays"] > 0 and st["extension_rays"] > 0
-    # the cost-ordered pixel fetch (on by default from 16 spp) forced on at 2 spp,
+    # the cost-ordered pixel fetch (on by default from 64 spp) forced on at 2 spp,
     # for k_path and for the deferred form this subset runs with by default
     try:
         for order, defer in ((1, 0), (2, 2)):
@@ -164,3 +166,86 @@ def test_c3_full_frame_split_invariance(c3):
     sel = sw > 0
     assert sel.sum() == m
     assert np.array_equal(sframe[sel], frame[sel])
+
+
+# Every render form of the library, as set_option values: (path, path_defer, path_order, count_tests).
+# The persistent kernels record per-pixel ray counts in their counting build only; the seed always.
+FORMS = [
+    ("k_path", dict(path=1, path_defer=0, path_order=0)),
+    ("k_path ordered", dict(path=1, path_defer=0, path_order=1)),
+    ("k_path_defer scrambled", dict(path=1, path_defer=1, path_order=0)),
+    ("k_path_defer ordered", dict(path=1, path_defer=1, path_order=2)),
+    ("wavefront", dict(path=0, path_defer=2, path_order=2)),
+]
+DEFAULTS = dict(path=2, path_defer=2, path_order=2, path_order_min_spp=64, count_tests=0, pixel_probe=0)
+
+
+def _render_forms(ctx, orc_rad, orc_w, orc_probe, tiles, spp, depth):
+    """Render `tiles` in every form (persistent ones also counted), each bit-exact in radiance and
+    weights, and in the per-pixel probe (final sampler state = every path length and RNG draw; ray
+    counts = every bounce and NEE decision) against the oracle.  Returns the forms whose ray counts
+    were compared."""
+    counted = []
+    try:
+        ctx.set_option("pixel_probe", 1)
+        ctx.set_option("path_order_min_spp", 0)
+        for name, opts in FORMS:
+            for count in ((0, 1) if opts["path"] == 1 else (0,)):
+                for k, v in opts.items():
+                    ctx.set_option(k, v)
+                ctx.set_option("count_tests", count)
+                what = f"{name}{' (counting build)' if count else ''}"
+                rad, w = ctx.render(spp, depth, tiles, W, H)
+                assert np.array_equal(w, orc_w), f"{what}: weights differ"
+                diff = np.abs(rad - orc_rad).max()
+                assert np.array_equal(rad, orc_rad), f"{what}: radiance differs (max abs diff {diff})"
+                pr = ctx.pixel_probe(dist.n_pixels(tiles))
+                if check_probe(pr, orc_probe, tiles, W, H, what):
+                    counted.append(what)
+    finally:
+        for k, v in DEFAULTS.items():
+            ctx.set_option(k, v)
+        ctx.reset_stats()
+    return counted
+
+
+def test_c3_integrator_probe_bit_exact(c3):
+    """Integrator parity on the headline scene that can fail on a shading bug: per pixel of the
+    strided subset, the final LCG state (its draw count encodes every path length, BSDF-pdf
+    rejection and light sample, sampler.h:54-67) and the closest-hit / shadow rays traced
+    (pathtracer.h:69-91, 133-164) equal the oracle's, for k_path and k_path_defer with and without the
+    cost-ordered fetch and for the wavefront."""
+    ctx, cs, orc, _ = c3
+    tiles = dist.tiles_for_rank(W, H, TILE, 0, 64)
+    orad, ow, st, opr = orc.render(2, 5, tiles=tiles, n_threads=16, probe=True)
+    ys, xs = np.nonzero(ow)
+    # the paths really bounce and sample lights here: the fingerprint is not trivially equal
+    assert opr["shadow_rays"][ys, xs].sum() > 0 and (opr["closest_rays"][ys, xs] > 2).mean() > 0.2
+    counted = _render_forms(ctx, orad, ow, opr, tiles, 2, 5)
+    assert len(counted) == 5, counted
+
+
+LIT_CAMERA = dict(position=(0.0, 1.4, 1.6), rotation=(0.0, -40.0, 0.0), fov=70.0)
+
+
+def test_c3_lit_view_render_bit_exact(c3):
+    """A lit test-only view of the same 10M-triangle SBVH soup: the camera sits under the emitter
+    (y = 1.5, facing down) looking down at the soup's top face, which the emitter lights, so NEE
+    contributions, emission at depth 0 and multi-bounce radiance all reach the film.  Strided tile
+    subset at 2 spp, every render form, bit-exact in radiance and in the per-pixel probe."""
+    ctx, cs, orc, _ = c3
+    cam = scene.PerspectiveCamera(resolution=(W, H), **LIT_CAMERA)
+    lit = dataclasses.replace(cs, camera=cam)
+    orc_lit = py_oracle.OracleScene(lit, orc.nodes, orc.tris, capi)
+    tiles = dist.tiles_for_rank(W, H, TILE, 5, 64)
+    ctx.set_camera(cam.position, cam.rotation, cam.fov, cam.resolution)
+    try:
+        orad, ow, st, opr = orc_lit.render(2, 5, tiles=tiles, n_threads=16, probe=True)
+        sel = ow > 0
+        L = orad.sum(-1)[sel] / 2
+        assert L.mean() > 0.2 and (L > 0).mean() > 0.3, f"view not lit: mean {L.mean()}, lit {(L > 0).mean()}"
+        counted = _render_forms(ctx, orad, ow, opr, tiles, 2, 5)
+        assert len(counted) == 5, counted
+    finally:
+        c = cs.camera
+        ctx.set_camera(c.position, c.rotation, c.fov, c.resolution)

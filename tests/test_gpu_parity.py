@@ -159,12 +159,23 @@ def test_trace_each_ray_once(hip_ctx_factory, n):
         assert 0 < c["shadow"]["rays"] <= 3 * 96 * 54
 
 
-def _check_render(ctx, orc, spp, depth, tiles, W, H, clamp=0.0, exact=False):
+def _check_render(ctx, orc, spp, depth, tiles, W, H, clamp=0.0, exact=False, probe=False):
+    """Render through the C-ABI and compare with the oracle bit for bit; with `probe`, also the
+    per-pixel fingerprint (final sampler state; ray counts where the form records them).  Returns
+    (radiance, weight), plus whether ray counts were compared when `probe`."""
+    if probe:
+        ctx.set_option("pixel_probe", 1)
     rad, w = ctx.render(spp, depth, tiles, W, H, ray_clamp=clamp, exact_cull=exact)
-    orad, ow, _ = orc.render(spp, depth, tiles=tiles, ray_clamp=clamp, exact_cull=exact)
+    out = orc.render(spp, depth, tiles=tiles, ray_clamp=clamp, exact_cull=exact, probe=probe)
+    orad, ow = out[0], out[1]
     assert np.array_equal(w, ow)
     bad = rad != orad
     assert not bad.any(), f"{bad.sum()} radiance values differ, max {np.abs(rad - orad).max()}"
+    if probe:
+        from helpers import slot_pixels, check_probe
+        ctx.set_option("pixel_probe", 0)
+        n = len(slot_pixels(tiles, W, H)[0])
+        return rad, w, check_probe(ctx.pixel_probe(n), out[3], tiles, W, H)
     return rad, w
 
 
@@ -519,6 +530,15 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
             W, H = cs.camera.resolution
             _check_render(ctx, orc, 5, 5, [(0, 0, W, H)], W, H)
             _check_render(ctx, orc, 9, 3, [(0, 0, W, H)], W, H)
+            # the per-pixel fingerprint (akr_pixel_probe): seeds always, ray counts from the
+            # wavefront and from the persistent kernels' counting build
+            try:
+                for count in (0, 1):
+                    ctx.set_option("count_tests", count)
+                    *_, rays = _check_render(ctx, orc, 3, 5, [(0, 0, W, H), (3, 1, 17, 9)], W, H, probe=True)
+                    assert rays == (path == 0 or count == 1)
+            finally:
+                ctx.set_option("count_tests", 0)
 
 
 @pytest.mark.parametrize("spp", [16, 32])

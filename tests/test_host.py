@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(capi.EXPORTS) == declared, "ctypes binding out of sync with include/akr_hip.h"
-    assert capi.load_library().akr_hip_api_version() == 1
+    assert capi.load_library().akr_hip_api_version() == 2
 
 
 def test_create_without_device_fails_cleanly():
@@ -235,6 +235,50 @@ def test_oracle_render_tiles_accumulate_and_threads():
     assert np.array_equal(full, r) and np.array_equal(wf, w)
     r2, w2, _ = orc.render(3, 5, tiles=part, radiance=r.copy(), weight=w.copy())
     assert np.array_equal(r2, 2 * full) and np.all(w2 == 6)
+
+
+def _lcg_draws(start, final, limit):
+    """Per pixel: LCG steps (kernel/sampler.h:54-67, s -> 1103515245 s + 12345 mod 2^32) from
+    `start` to `final`, or -1 if not reached within `limit`."""
+    s = start.astype(np.uint64)
+    f = final.astype(np.uint64)
+    out = np.full(s.shape, -1, np.int64)
+    for k in range(limit + 1):
+        out[(out < 0) & (s == f)] = k
+        s = (s * 1103515245 + 12345) & 0xFFFFFFFF
+    return out
+
+
+@pytest.mark.parametrize("depth", [0, 1, 5])
+def test_oracle_pixel_probe_properties(depth):
+    """The oracle's per-pixel fingerprint (orc_render_probe, the checker of the GPU pixel probe):
+    the final sampler state lies 4 + 6k (+2 per zero-pdf BSDF sample) draws per sample after the
+    pixel's seed x + y W (pathtracer.h:61-131), closest-hit traces count the camera ray plus every
+    extension ray below max_depth, NEE shadow rays at most one per scatter.  max_depth 0 / 1 pin the
+    counts exactly; the probe does not change the image."""
+    W, H, spp = 24, 16, 3
+    cs = scene.compile_scene(cornell((W, H)))
+    nodes, tris, _ = capi.build_bvh_host(cs.vertices, cs.indices)
+    orc = O.OracleScene(cs, nodes, tris, capi)
+    r0, w0, _ = orc.render(spp, depth)
+    r, w, st, pr = orc.render(spp, depth, probe=True)
+    assert np.array_equal(r, r0) and np.array_equal(w, w0)
+    assert np.all(pr["flags"] == (capi.PROBE_SEED | capi.PROBE_RAYS))
+    ys, xs = np.mgrid[0:H, 0:W]
+    draws = _lcg_draws((xs + ys * W).reshape(-1), pr["seed"].reshape(-1), spp * (6 + 6 * depth))
+    assert np.all(draws >= 4 * spp) and np.all((draws - 4 * spp) % 2 == 0)
+    cl, sh = pr["closest_rays"].reshape(-1), pr["shadow_rays"].reshape(-1)
+    scatter_draws = draws - 4 * spp
+    assert st["camera_rays"] <= cl.sum() <= st["camera_rays"] + st["extension_rays"]
+    assert sh.sum() == st["shadow_rays"]
+    if depth == 0:
+        assert np.all(cl == spp) and np.all(sh == 0) and np.all(draws == 4 * spp)
+    else:
+        assert np.all(cl >= spp) and np.all(cl <= spp * max(1, depth))
+        assert np.all(6 * (cl - spp) <= scatter_draws) and np.all(sh <= scatter_draws // 6)
+        assert sh.sum() > 0
+    if depth == 1:
+        assert np.all(cl == spp)   # the trace at depth == max_depth adds nothing and is not made
 
 
 def test_oracle_overlapping_tiles_merge_in_tile_order():
