@@ -215,12 +215,17 @@ def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost
     return nodes, tris, info
 
 
-def render_node(ctxs, spp, max_depth, tiles, width, height, ray_clamp=0.0, exact_cull=False):
+def render_node(ctxs, spp, max_depth, tiles, width, height, ray_clamp=0.0, exact_cull=False, radiance=None,
+                weight=None):
     """akr_hip_render_node: tile j on ctxs[j % len(ctxs)], one host thread per context; returns
-    the full-frame (radiance, weight) accumulated like HipContext.render."""
+    the full-frame (radiance, weight) accumulated like HipContext.render (into the given buffers)."""
     lib = load_library()
-    radiance = np.zeros((height, width, 3), np.float32)
-    weight = np.zeros((height, width), np.float32)
+    if radiance is None:
+        radiance = np.zeros((height, width, 3), np.float32)
+    if weight is None:
+        weight = np.zeros((height, width), np.float32)
+    assert radiance.dtype == np.float32 and radiance.flags.c_contiguous and radiance.size == 3 * width * height
+    assert weight.dtype == np.float32 and weight.flags.c_contiguous and weight.size == width * height
     arr = (Rect * max(1, len(tiles)))(*[Rect(*t) for t in tiles])
     hs = (C.c_void_p * len(ctxs))(*[c.h for c in ctxs])
     p = PtParams(int(spp), int(max_depth), float(ray_clamp), PT_EXACT_CULL if exact_cull else 0)

@@ -285,8 +285,10 @@ struct akr_hip_ctx {
     DBuf<akr_hit> d_trace_hits;
     // akr_hip_render_node on the lead context: the frame and the staging of other contexts' films
     DBuf<float> d_frame;
-    DBuf<float4> d_gfilm;
-    DBuf<uint32_t> d_gpix, d_gorder;
+    std::vector<std::unique_ptr<DBuf<float4>>> g_film;     // [k]: context k's packed film (staging)
+    std::vector<std::unique_ptr<DBuf<uint32_t>>> g_pix;    // [k]: its pixel list
+    DBuf<uint32_t> d_gorder;                               // merge orders of overlapping tiles
+    hipEvent_t ev_gather = nullptr;  // this context's push to the lead device is done
 
     // instrumentation
     bool stats = false, count = false;
@@ -326,6 +328,7 @@ struct akr_hip_ctx {
         if (h_check) (void)hipHostFree(h_check);
         if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
+        if (ev_gather) (void)hipEventDestroy(ev_gather);
         if (main_st) (void)hipStreamDestroy(main_st);
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1467,6 +1470,12 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
         lead->err = "null or invalid argument";
         return -1;
     }
+    for (int32_t k = 0; k < n_ctx; k++)
+        for (int32_t j = 0; j < k; j++)
+            if (ctxs[j] == ctxs[k]) {  // the per-context render threads would share one context
+                lead->err = "a context is listed twice";
+                return -1;
+            }
     // tile j -> context j % n_ctx (interleaved, like the multi-process split of akari_amd/dist.py);
     // one host thread per context, each bound to its device by guard()
     std::vector<std::vector<akr_rect>> part(n_ctx);
@@ -1493,9 +1502,12 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
             if (k) lead->err = "context " + std::to_string(k) + ": " + ctxs[k]->err;
             return -1;
         }
-    // Gather on the lead device (Film::merge_tile, core/film.h:85-95): each context's packed film
-    // and pixel list are copied device to device (over xGMI between GPUs), and k_merge_film adds them
-    // into the frame in context order; the frame goes to the host once.
+    // Gather on the lead device (Film::merge_tile, core/film.h:85-95).  Every other context pushes its
+    // packed film and pixel list into its own staging buffers on the lead device from its own stream
+    // (device-to-device peer copies, over xGMI between GPUs), so the copies of all contexts run at
+    // once; the lead stream waits for each context's copy event and k_merge_film adds the films into
+    // the frame in context order (the host loop's order).  No host synchronisation until the frame
+    // goes back to the host.
     return guard(lead, [&] {
         const int W = lead->cam.width, H = lead->cam.height;
         const uint64_t F = (uint64_t)W * (uint64_t)H;
@@ -1510,48 +1522,83 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
         float *frad = lead->d_frame.p, *fw = lead->d_frame.p + 3 * F;
         HIPCHK(hipMemcpyAsync(frad, radiance, 3 * F * sizeof(float), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(fw, weight, F * sizeof(float), hipMemcpyHostToDevice, st));
-        std::vector<uint16_t> seen;
+        // a pixel listed r times by one context (overlapping tiles) goes to its r-th launch, so the
+        // adds of a pixel stay in list order and no launch adds one pixel twice
+        std::vector<uint32_t> seen(F, 0), all_order;
+        std::vector<std::vector<std::pair<size_t, uint32_t>>> launches(n_ctx);  // (offset, count) per rank
         for (int32_t k = 0; k < n_ctx; k++) {
-            akr_hip_ctx *c = ctxs[k];
             const uint64_t N = npix[k];
             if (N == 0) continue;
-            const float4 *film = c->d_film.p;
-            const uint32_t *pix = c->d_pixel.p;
-            if (c != lead) {
-                HIPCHK(hipStreamWaitEvent(st, c->ev_done, 0));
-                lead->d_gfilm.reserve(N);
-                lead->d_gpix.reserve(N);
-                HIPCHK(hipMemcpyPeerAsync(lead->d_gfilm.p, lead->device, c->d_film.p, c->device, N * sizeof(float4), st));
-                HIPCHK(hipMemcpyPeerAsync(lead->d_gpix.p, lead->device, c->d_pixel.p, c->device, N * sizeof(uint32_t), st));
-                film = lead->d_gfilm.p;
-                pix = lead->d_gpix.p;
-            }
-            // a pixel listed twice (overlapping tiles) goes to successive launches, in list order
-            seen.assign(F, 0);
+            std::fill(seen.begin(), seen.end(), 0u);
             std::vector<std::vector<uint32_t>> rank;
             for (uint64_t i = 0; i < N; i++) {
-                const uint32_t px = c->h_pixel[i];
+                const uint32_t px = ctxs[k]->h_pixel[i];
                 const uint64_t p = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
-                const uint16_t r = seen[p]++;
+                const uint32_t r = seen[p]++;
                 if (r >= rank.size()) rank.emplace_back();
                 rank[r].push_back((uint32_t)i);
             }
             if (rank.size() == 1) {
-                launch_merge_film(film, pix, nullptr, (uint32_t)N, W, frad, fw, st);
-            } else {
-                for (auto &ord : rank) {
-                    lead->d_gorder.upload(ord.data(), ord.size(), st);
-                    launch_merge_film(film, pix, lead->d_gorder.p, (uint32_t)ord.size(), W, frad, fw, st);
-                    HIPCHK(hipStreamSynchronize(st));  // d_gorder is reused by the next launch
-                }
+                launches[k].push_back({SIZE_MAX, (uint32_t)N});  // identity order
+                continue;
             }
+            for (auto &ord : rank) {
+                launches[k].push_back({all_order.size(), (uint32_t)ord.size()});
+                all_order.insert(all_order.end(), ord.begin(), ord.end());
+            }
+        }
+        if (!all_order.empty()) lead->d_gorder.upload(all_order.data(), all_order.size(), st);
+        // the peer pushes: one staging pair per context on the lead device, each copy on its
+        // context's stream after that context's render
+        if (lead->g_film.size() < (size_t)n_ctx) {
+            lead->g_film.resize(n_ctx);
+            lead->g_pix.resize(n_ctx);
+        }
+        for (int32_t k = 1; k < n_ctx; k++) {
+            akr_hip_ctx *c = ctxs[k];
+            const uint64_t N = npix[k];
+            if (N == 0 || c == lead) continue;
+            if (!lead->g_film[k]) {
+                lead->g_film[k].reset(new DBuf<float4>());
+                lead->g_pix[k].reset(new DBuf<uint32_t>());
+            }
+            lead->g_film[k]->reserve(N);  // on the lead device (current)
+            lead->g_pix[k]->reserve(N);
+            HIPCHK(hipSetDevice(c->device));
+            if (!c->ev_gather) HIPCHK(hipEventCreateWithFlags(&c->ev_gather, hipEventDisableTiming));
+            HIPCHK(hipMemcpyPeerAsync(lead->g_film[k]->p, lead->device, c->d_film.p, c->device, N * sizeof(float4),
+                                      c->stream));
+            HIPCHK(hipMemcpyPeerAsync(lead->g_pix[k]->p, lead->device, c->d_pixel.p, c->device, N * sizeof(uint32_t),
+                                      c->stream));
+            HIPCHK(hipEventRecord(c->ev_gather, c->stream));
+            c->mark_done(c->stream);  // the context's film is not reused before the copy is done
+            HIPCHK(hipSetDevice(lead->device));
+        }
+        for (int32_t k = 0; k < n_ctx; k++) {
+            akr_hip_ctx *c = ctxs[k];
+            if (npix[k] == 0) continue;
+            const float4 *film = c->d_film.p;
+            const uint32_t *pix = c->d_pixel.p;
+            if (c != lead) {
+                HIPCHK(hipStreamWaitEvent(st, c->ev_gather, 0));
+                film = lead->g_film[k]->p;
+                pix = lead->g_pix[k]->p;
+            }
+            for (const auto &l : launches[k])
+                launch_merge_film(film, pix, l.first == SIZE_MAX ? nullptr : lead->d_gorder.p + l.first, l.second, W,
+                                  frad, fw, st);
             HIPCHK(hipGetLastError());
-            if (c != lead) HIPCHK(hipStreamSynchronize(st));  // the staging buffers are reused
         }
         HIPCHK(hipMemcpyAsync(radiance, frad, 3 * F * sizeof(float), hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(weight, fw, F * sizeof(float), hipMemcpyDeviceToHost, st));
         lead->mark_done(st);
         HIPCHK(hipStreamSynchronize(st));
+        for (int32_t k = 1; k < n_ctx; k++)  // a context's next call orders after its copy anyway
+            if (ctxs[k] != lead && npix[k]) {
+                HIPCHK(hipSetDevice(ctxs[k]->device));
+                HIPCHK(hipStreamSynchronize(ctxs[k]->stream));
+            }
+        HIPCHK(hipSetDevice(lead->device));
     });
 }
 

@@ -319,6 +319,30 @@ def test_render_node_matches_single_context(hip_ctx_factory):
         assert np.array_equal(rad, orad)
 
 
+def test_render_node_overlapping_tiles_prefilled(hip_ctx_factory):
+    """render_node with three contexts, overlapping and repeated tiles (a pixel listed up to 8 times,
+    several times by one context: the gather's per-rank merge launches) into pre-filled host
+    buffers: the single-context result bit for bit, and the oracle's."""
+    with hip_ctx_factory(0) as a, hip_ctx_factory(0) as b, hip_ctx_factory(0) as c:
+        sc = cornell((40, 24))
+        cs, orc = _setup(a, sc)
+        scene.upload_scene(b, cs)
+        scene.upload_scene(c, cs)
+        t = (4, 2, 20, 14)
+        tiles = [t, (0, 0, 40, 24), t, (10, 5, 30, 20), t, t, (16, 0, 32, 8), t, (-5, -5, 3, 3)]
+        rng = np.random.default_rng(7)
+        pre_r = rng.uniform(0, 3, (24, 40, 3)).astype(np.float32)
+        pre_w = rng.integers(0, 5, (24, 40)).astype(np.float32)
+        ref, wref = a.render(3, 5, tiles, 40, 24, radiance=pre_r.copy(), weight=pre_w.copy())
+        rad, w = capi.render_node([a, b, c], 3, 5, tiles, 40, 24, radiance=pre_r.copy(), weight=pre_w.copy())
+        assert np.array_equal(w, wref) and np.array_equal(rad, ref)
+        orad, ow, _ = orc.render(3, 5, tiles=tiles, radiance=pre_r.copy(), weight=pre_w.copy())
+        assert np.array_equal(w, ow) and np.array_equal(rad, orad)
+        assert (w - pre_w)[5, 16] == 8 * 3   # listed 8 times: t x 5, the frame, two more tiles
+        with pytest.raises(capi.AkrError):   # one context listed twice would race with itself
+            capi.render_node([a, b, a], 3, 5, tiles, 40, 24)
+
+
 def test_render_device_packed(hip_ctx_factory):
     torch = pytest.importorskip("torch")
     with hip_ctx_factory(0) as ctx:
