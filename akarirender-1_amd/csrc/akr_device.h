@@ -293,6 +293,8 @@ struct PathArgs {
                                    // shadow result (parity * 8 + bounce), then the waiting extension ray
     uint32_t mix;                  // k_path_defer: scrambled pixel order within each XCD shard
     const uint32_t *order;         // optional: fetch index -> slot (cost-ordered fetch)
+    uint32_t order_mode;           // with `order`: FETCH_LINEAR (costliest first) or FETCH_PAIR (kernels.hip)
+    uint32_t prio;                 // 0, or: waves fetching in the first prio/256 of a shard raise their priority
     uint4 *probe;                  // optional, per slot (akr_pixel_probe): final sampler state; the counting
                                    // build adds the pixel's closest-hit and shadow rays
     uint32_t *fault;               // mapped host word: set when a wave stops on the hang guard (k_path_defer)

@@ -260,6 +260,14 @@ struct akr_hip_ctx {
     // pilot costs about one third of a sample pass); classes
     // of 2^path_order_shift pilot steps.  Measured on C3 at 64 spp: 2- / 4- / 8-way shares 2-5 % faster
     int path_order = 2;
+    // option "path_order_pair": the cost-ordered fetch of k_path_defer pairs each shard's costliest
+    // pixels with its cheapest inside a wave (lanes done early take the long pixels' shadow rays)
+    // instead of costliest-first: 1 = on, 0 = off, 2 (default) = on for renders of at most 400 K
+    // pixels (measured on C3 at 32 spp, DESIGN.md §3.10: 8-way share 1.007 -> 0.946 ms, 4-way share
+    // 1.499 -> 1.548 ms); option "path_prio": waves whose pixels lie in the first path_prio / 256 of
+    // a cost-ordered shard run at raised issue priority (0 = off; measured without effect)
+    int path_order_pair = 2;
+    int path_prio = 0;
     int path_order_min_spp = 64;
     int path_order_shift = 2;
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
@@ -930,6 +938,9 @@ struct akr_hip_ctx {
                 if (path_order != 0 && (!defer || path_order == 2) && p.spp >= path_order_min_spp && N >= 2) {
                     timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
                     pa.order = d_oidx[1].p;
+                    const bool pair = defer && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000));
+                    pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
+                    pa.prio = (uint32_t)path_prio;
                 }
                 timed("path", ms, [&] { launch_path(count, defer, tab, pa, grid, ms); });
                 HIPCHK(hipGetLastError());
@@ -1237,6 +1248,12 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_shift") {
             if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
             ctx->path_order_shift = (int)value;
+        } else if (k == "path_order_pair") {
+            if (value < 0 || value > 2) throw std::runtime_error("path_order_pair must be 0, 1 or 2 (auto)");
+            ctx->path_order_pair = (int)value;
+        } else if (k == "path_prio") {
+            if (value < 0 || value > 256) throw std::runtime_error("path_prio must be in [0, 256]");
+            ctx->path_prio = (int)value;
         } else if (k == "path_mix") {
             ctx->path_mix = value != 0;
         } else if (k == "path_tab") {

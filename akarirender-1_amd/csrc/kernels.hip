@@ -1554,16 +1554,23 @@ __device__ __forceinline__ void path_unpark(uint32_t (*s_park)[kTraceBlock], uin
                                             bool occl);
 
 // Wave-level pixel fetch from the XCD shards (k_trace's refill): every lane with `need` set gets
-// the next pixel of its wave's shard, or `done` once every shard is exhausted.  With `mix` the
-// fetch order is scrambled within each shard ((i * (2^31 - 1)) mod len, a bijection): the lanes of a
-// wave then hold pixels from all over their shard instead of one tile's rows.
+// the next pixel of its wave's shard, or `done` once every shard is exhausted.  Fetch index i of a
+// shard maps to its slot by `mode`: FETCH_LINEAR (i), FETCH_SCRAMBLE ((i * (2^31 - 1)) mod len, a
+// bijection: the lanes of a wave hold pixels from all over their shard instead of one tile's rows),
+// or FETCH_PAIR (i/2 from the front for even i, from the back for odd i: over a cost-ordered shard
+// each wave holds the costliest and the cheapest pixels left, so lanes whose pixel ends early can
+// take the long pixels' shadow rays).  `order` (optional) maps the position to the
+// slot.  With `prio`, a wave whose fetch lies in the first `prio` / 256 of its shard (the costliest
+// pixels of a cost order) raises its issue priority, else lowers it.
+enum : uint32_t { FETCH_LINEAR = 0, FETCH_SCRAMBLE = 1, FETCH_PAIR = 2 };
 struct PixelFetch {
     uint32_t shard, s_lo, s_hi;
     int shards_left;
     bool drained;
 };
-__device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t *work, bool mix,
-                                             const uint32_t *order, bool &need, bool &done, uint32_t &pix) {
+__device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t *work, uint32_t mode,
+                                             const uint32_t *order, uint32_t prio, bool &need, bool &done,
+                                             uint32_t &pix) {
     while (true) {
         const unsigned long long want = __ballot(need && !done);
         if (want == 0) break;
@@ -1575,17 +1582,24 @@ __device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t
         const int leader = __ffsll((long long)want) - 1;
         uint32_t base = 0;
         if ((int)__lane_id() == leader) base = atomicAdd(work + f.shard * kWorkStride, nw);
-        base = __shfl(base, leader);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+        const uint32_t len = f.s_hi - f.s_lo;
+        if (prio && base < len) {  // wave-uniform
+            if ((uint64_t)base * 256u < (uint64_t)len * prio) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if (need && !done) {
             const uint32_t my = base + lane_prefix(want);
-            const uint32_t len = f.s_hi - f.s_lo;
             if (base < len && my < len) {
-                const uint32_t at = f.s_lo + (mix ? (uint32_t)(((uint64_t)my * 2147483647ull) % len) : my);
+                uint32_t pos = my;
+                if (mode == FETCH_SCRAMBLE) pos = (uint32_t)(((uint64_t)my * 2147483647ull) % len);
+                else if (mode == FETCH_PAIR) pos = (my & 1u) ? len - 1u - (my >> 1) : (my >> 1);
+                const uint32_t at = f.s_lo + pos;
                 pix = order ? order[at] : at;
                 need = false;
             }
         }
-        if (base + nw >= f.s_hi - f.s_lo) {  // this shard is exhausted: move to the next open one
+        if (base + nw >= len) {  // this shard is exhausted: move to the next open one
             while (true) {
                 if (--f.shards_left == 0) {
                     f.drained = true;
@@ -1788,7 +1802,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             }
             // next pixel for the lanes that finished theirs: one atomic per wave per attempt
             const bool asked = need_pixel && !done;
-            fetch_pixels(f, n, pa.work, false, pa.order, need_pixel, done, pix);
+            fetch_pixels(f, n, pa.work, pa.order ? pa.order_mode : FETCH_LINEAR, pa.order, pa.prio, need_pixel, done, pix);
             if (asked && !need_pixel) {
                 const uint32_t px = pa.pixel[pix];
                 left = pa.spp;
@@ -2095,7 +2109,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 need_pixel = true;
             }
             const bool asked = need_pixel && !done;
-            fetch_pixels(f, n, pa.work, pa.mix != 0 && !pa.order, pa.order, need_pixel, done, pix);  // the cost order replaces the scramble
+            fetch_pixels(f, n, pa.work, pa.order ? pa.order_mode : (pa.mix ? FETCH_SCRAMBLE : FETCH_LINEAR), pa.order, pa.prio,
+                         need_pixel, done, pix);  // the cost order replaces the scramble
             if (asked && !need_pixel) {
                 pxy = pa.pixel[pix];
                 left = pa.spp;

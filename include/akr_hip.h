@@ -253,7 +253,12 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
                         const akr_rect *tiles, int32_t n_tiles, float *radiance, float *weight);
 /* Same, but writes (overwrites) device buffers in packed tile order: pixel k of the tile list
  * (tiles in order, row-major inside a tile) -> radiance[3k..3k+2], weight[k].  Returns the
- * pixel count in *n_pixels.  Asynchronous on `stream`. */
+ * pixel count in *n_pixels.  The work is enqueued on `stream`; with option "verify" on (the
+ * default) the call then WAITS on the host for the render and its in-band check (every slot holds
+ * spp samples, and no persistent wave stopped on its hang guard) before it returns, so the check
+ * can fail this call.  With "verify" 0 the call returns once the work is enqueued (fully
+ * asynchronous); a hang-guard fault is then reported by the context's next render or
+ * akr_hip_synchronize. */
 int akr_hip_render_device(akr_hip_ctx *ctx, const akr_pt_params *params, const akr_rect *tiles,
                           int32_t n_tiles, float *d_radiance, float *d_weight, void *stream,
                           uint64_t *n_pixels);

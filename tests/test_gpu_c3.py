@@ -174,10 +174,12 @@ FORMS = [
     ("k_path", dict(path=1, path_defer=0, path_order=0)),
     ("k_path ordered", dict(path=1, path_defer=0, path_order=1)),
     ("k_path_defer scrambled", dict(path=1, path_defer=1, path_order=0)),
-    ("k_path_defer ordered", dict(path=1, path_defer=1, path_order=2)),
+    ("k_path_defer ordered", dict(path=1, path_defer=1, path_order=2, path_order_pair=0)),
+    ("k_path_defer ordered, paired", dict(path=1, path_defer=1, path_order=2, path_order_pair=1)),
     ("wavefront", dict(path=0, path_defer=2, path_order=2)),
 ]
-DEFAULTS = dict(path=2, path_defer=2, path_order=2, path_order_min_spp=64, count_tests=0, pixel_probe=0)
+DEFAULTS = dict(path=2, path_defer=2, path_order=2, path_order_pair=2, path_order_min_spp=64, count_tests=0,
+                pixel_probe=0)
 
 
 def _render_forms(ctx, orc_rad, orc_w, orc_probe, tiles, spp, depth):
@@ -222,7 +224,7 @@ def test_c3_integrator_probe_bit_exact(c3):
     # the paths really bounce and sample lights here: the fingerprint is not trivially equal
     assert opr["shadow_rays"][ys, xs].sum() > 0 and (opr["closest_rays"][ys, xs] > 2).mean() > 0.2
     counted = _render_forms(ctx, orad, ow, opr, tiles, 2, 5)
-    assert len(counted) == 5, counted
+    assert len(counted) == 6, counted
 
 
 LIT_CAMERA = dict(position=(0.0, 1.4, 1.6), rotation=(0.0, -40.0, 0.0), fov=70.0)
@@ -245,7 +247,7 @@ def test_c3_lit_view_render_bit_exact(c3):
         L = orad.sum(-1)[sel] / 2
         assert L.mean() > 0.2 and (L > 0).mean() > 0.15, f"view not lit: mean {L.mean()}, lit {(L > 0).mean()}"
         counted = _render_forms(ctx, orad, ow, opr, tiles, 2, 5)
-        assert len(counted) == 5, counted
+        assert len(counted) == 6, counted
     finally:
         c = cs.camera
         ctx.set_camera(c.position, c.rotation, c.fov, c.resolution)

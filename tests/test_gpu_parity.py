@@ -535,6 +535,7 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
         ctx.set_option("path_order", order)
+        ctx.set_option("path_order_pair", 1 if (order == 2 and defer) else 0)   # paired cost order (§3.10)
         ctx.set_option("path_order_min_spp", 0 if order else 64)
         ctx.set_option("path_order_shift", 0)
     with hip_ctx_factory(0) as ctx:

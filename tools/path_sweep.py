@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--scene", choices=["soup", "hall", "cornell"], default="soup")
     ap.add_argument("--profile", type=int, default=0, help="also print the counted k_path phase profile")
     ap.add_argument("--splits", default="8", help="emulated ranks of the tile split to time besides the full frame")
+    ap.add_argument("--opts", default="", help="extra library options to sweep: 'key=v1,v2;key2=v1,v2' (cartesian)")
     args = ap.parse_args()
     libs = args.libs.split(",")
     if len(libs) > 1:
@@ -76,7 +77,13 @@ def main():
                   for d in (int(x) for x in args.defer.split(",")) for m in (int(x) for x in args.mix.split(","))
                   for t in (int(x) for x in args.tab.split(",")) for o in (int(x) for x in args.order.split(","))
                   for osh in (int(x) for x in args.order_shift.split(","))]
-        for path, ff, dfr, mx, tab, order, osh in combos:
+        import itertools
+        extra = [(kv.split("=")[0], [int(x) for x in kv.split("=")[1].split(",")]) for kv in args.opts.split(";") if kv]
+        extra_combos = list(itertools.product(*[[(k, v) for v in vs] for k, vs in extra])) or [()]
+        combos = [c + (e,) for c in combos for e in extra_combos]
+        for path, ff, dfr, mx, tab, order, osh, ex in combos:
+            for k, v in ex:
+                ctx.set_option(k, v)
             ctx.set_option("path_order", order)
             ctx.set_option("path_order_shift", osh)
             ctx.set_option("path_tab", tab)
@@ -96,7 +103,8 @@ def main():
                     ctx.render_device(args.steps, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
                     torch.cuda.synchronize(dev)
                     res.append((time.perf_counter() - t) / args.steps * 1e3)
-                print(f"   path={path} far_first={ff} defer={dfr} mix={mx} tab={tab} order={order}/{osh} min_wait={mw} grid={gp}%: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
+                print(f"   path={path} far_first={ff} defer={dfr} mix={mx} tab={tab} order={order}/{osh} min_wait={mw} grid={gp}%"
+                      f"{''.join(f' {k}={v}' for k, v in ex)}: full {res[0]:.3f} ms/step ({W * H / res[0] / 1e3:.1f} Msamples/s)"
                       + "".join(f", {n}-way rank {r:.3f} ms/step (projected {res[0] / r:.2f}x, {W * H / r / 1e3:.0f} Msamples/s)"
                                 for n, r in zip(splits, res[1:])), flush=True)
                 if args.profile and path:
