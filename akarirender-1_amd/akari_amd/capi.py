@@ -164,7 +164,10 @@ def load_library() -> C.CDLL:
         if not LIB_PATH.exists():
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
         lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+        variant = "AKR_HIP_LIB" in os.environ  # an A/B build may predate newer exports
         for name, (res, args) in EXPORTS.items():
+            if variant and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -10,7 +10,8 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-KERNELS = {"k_path<false>": "path (k_path)", "k_trace<0, false, true, true>": "closest (k_trace)",
+KERNELS = {"k_path<false>": "path (k_path)", "k_path<false, true>": "path (k_path, LDS tables)",
+           "k_path_defer<false, true>": "path (k_path_defer, LDS tables)", "k_trace<0, false, true, true>": "closest (k_trace)",
            "k_trace<2, false, true, true>": "shadow (k_trace)", "k_shade": "shade (k_shade)"}
 
 
@@ -57,8 +58,8 @@ def main(tag):
         out += [f"## render form: {'persistent path kernel' if path else 'wavefront'} (bench --path {path})", "",
                 "| kernel | launches | VGPR | LDS B | waves | wave-cycles | parked (WAIT_ANY) | issue-stall (WAIT_INST_ANY) | "
                 "issuing (ACTIVE_INST_ANY) | VALU active / wave-cycles | VALU insts / wave | LDS insts / wave | "
-                "VMEM rd / wave | SALU / wave | HBM MB / launch | L2 hit % | clock GHz |",
-                "|" + "---|" * 17]
+                "VMEM rd / wave | VMEM wr / wave | SALU / wave | HBM MB / launch | read MB | write MB | L2 hit % |",
+                "|" + "---|" * 19]
         for k, c in vals.items():
             m = lambda n: (sum(c[n]) / len(c[n])) if c.get(n) else float("nan")
             waves = m("SQ_WAVES")
@@ -67,19 +68,20 @@ def main(tag):
             hit, miss = m("TCC_HIT_sum"), m("TCC_MISS_sum")
             traffic[k] = {"hbm_bytes_per_launch": hbm, "read_bytes": 2 * m("FETCH_SIZE") * 1024,
                           "write_bytes": m("WRITE_SIZE") * 1024, "launches_sampled": len(c.get("FETCH_SIZE", []))}
-            if k == "k_path<false>" and spp_total:   # one launch renders every spp: bytes per sample pass
+            if k.startswith("k_path") and spp_total:   # one launch renders every spp: bytes per sample pass
                 n = len(c.get("FETCH_SIZE", []))
                 traffic[k]["hbm_bytes_per_spp"] = hbm * n / spp_total
             out.append(f"| {KERNELS[k]} | {len(c.get('SQ_WAVES', []))} | {meta[k]['vgpr']} | {meta[k]['lds']} | {waves:.0f} | "
                        f"{wc:.3g} | {m('SQ_WAIT_ANY') / wc:.3f} | {m('SQ_WAIT_INST_ANY') / wc:.3f} | "
                        f"{m('SQ_ACTIVE_INST_ANY') / wc:.3f} | {m('SQ_ACTIVE_INST_VALU') / wc:.3f} | "
                        f"{m('SQ_INSTS_VALU') / waves:.3g} | {m('SQ_INSTS_LDS') / waves:.3g} | "
-                       f"{m('SQ_INSTS_VMEM_RD') / waves:.3g} | {m('SQ_INSTS_SALU') / waves:.3g} | {hbm / 1e6:.1f} | "
-                       f"{100 * hit / (hit + miss):.1f} | "
-                       f"{m('GRBM_GUI_ACTIVE') / 8 / max(1e-9, 1.0):.3g} |")
+                       f"{m('SQ_INSTS_VMEM_RD') / waves:.3g} | {m('SQ_INSTS_VMEM_WR') / waves:.3g} | "
+                       f"{m('SQ_INSTS_SALU') / waves:.3g} | {hbm / 1e6:.1f} | {2 * m('FETCH_SIZE') * 1024 / 1e6:.1f} | "
+                       f"{m('WRITE_SIZE') * 1024 / 1e6:.1f} | {100 * hit / (hit + miss):.1f} |")
         out.append("")
-    out += ["Fractions are of SQ_WAVE_CYCLES (quad-cycles summed over waves); the clock column is GRBM_GUI_ACTIVE / 8 "
-            "(cycles per XCD, divide by the kernel time for the clock).", ""]
+    out += ["Fractions are of SQ_WAVE_CYCLES (quad-cycles summed over waves).  A persistent path launch renders "
+            "every spp of its render: the bench's launches are the warmup, the timed K-spp render and the "
+            "min(K, 4)-spp breakdown pass, and traffic.json's hbm_bytes_per_spp divides by their spp sum.", ""]
     dst = ROOT / "profiles"
     (dst / f"{tag}_pmc.md").write_text("\n".join(out) + "\n")
     (dst / f"{tag}_traffic.json").write_text(json.dumps(
