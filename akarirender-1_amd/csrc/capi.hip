@@ -285,8 +285,8 @@ struct akr_hip_ctx {
     bool serial_shadow = false;  // option "serial_shadow": wavefront shadow traces on the main stream (isolated timing)
     bool any_far_first = false;  // option "any_far_first": shadow traversal visits far slots first (measured: more visits on C3)
     // option "path_min_wait": a persistent kernel's wave processes its waiting lanes once this many of
-    // 64 wait (scaled to the wave's live lanes); 0 (default) = 32 for k_path_defer renders of at most
-    // 400 K pixels (an 8-way share), 40 otherwise (measured on C3)
+    // 64 wait (scaled to the wave's live lanes); 0 (default) = 40 (measured on C3, DESIGN.md §3.8: with
+    // the paired order the 8-way share runs 0.944-0.948 ms at 40, 0.972 at 32, 1.007 at 56)
     int path_min_wait = 0;
     int path_grid_pct = 100;  // option "path_grid_pct": persistent path grid as a percentage of the resident maximum
     DBuf<float4> d_trace_rays;
@@ -923,7 +923,7 @@ struct akr_hip_ctx {
                 const uint64_t resident = (uint64_t)path_grid[defer][tab] * (uint64_t)path_grid_pct / 100;
                 const uint32_t grid = (uint32_t)std::max<uint64_t>(
                     1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
-                pa.min_wait = (uint32_t)(path_min_wait > 0 ? path_min_wait : (defer && N <= 400000) ? 32 : 40);
+                pa.min_wait = (uint32_t)(path_min_wait > 0 ? path_min_wait : 40);
                 if (defer) {
                     d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
                     pa.contrib = d_contrib.p;
