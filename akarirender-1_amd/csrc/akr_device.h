@@ -298,6 +298,7 @@ struct PathArgs {
     uint4 *probe;                  // optional, per slot (akr_pixel_probe): final sampler state; the counting
                                    // build adds the pixel's closest-hit and shadow rays
     uint32_t *fault;               // mapped host word: set when a wave stops on the hang guard (k_path_defer)
+    uint32_t fault_test;           // test only: k_path_defer raises `fault` once at the end of the launch
 };
 
 }  // namespace akr

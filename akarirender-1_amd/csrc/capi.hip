@@ -166,6 +166,7 @@ struct akr_hip_ctx {
     uint32_t *h_fault = nullptr, *d_fault_host = nullptr;
     // Test-only per-slot fingerprint of the last render (option "pixel_probe", akr_pixel_probe)
     bool probe = false;
+    bool fault_test = false;  // option "fault_test": k_path_defer raises the fault word once (tests)
     DBuf<uint4> d_probe;
     uint64_t probe_n = 0;
     bool probe_ok = false;
@@ -916,6 +917,7 @@ struct akr_hip_ctx {
                 pa.prof = count ? d_pprof.p : nullptr;
                 pa.probe = probe_p;
                 pa.fault = d_fault_host;
+                pa.fault_test = fault_test ? 1u : 0u;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
                 // the shading's material / light / CDF tables in LDS when they fit
@@ -1266,6 +1268,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_min_wait = (int)value;
         } else if (k == "pixel_probe") {
             ctx->probe = value != 0;
+        } else if (k == "fault_test") {
+            ctx->fault_test = value != 0;
         } else if (k == "verify") {
             ctx->verify = value != 0;
         } else if (k == "la_early_exit") {

@@ -2214,6 +2214,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         if (COUNT) p_tl += wall_clock64() - p_t;
     }
     if (COUNT) path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
+    // test-only (option "fault_test"): raise the hang guard's fault word once, so the host-side
+    // reporting path can be exercised without a hang
+    if (pa.fault_test && pa.fault && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_or(pa.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Film::merge_tile (core/film.h:85-95) on the device: a context's packed film (one float4 per

@@ -343,6 +343,33 @@ def test_render_node_overlapping_tiles_prefilled(hip_ctx_factory):
             capi.render_node([a, b, a], 3, 5, tiles, 40, 24)
 
 
+def test_hang_guard_fault_is_reported(hip_ctx_factory):
+    """The persistent kernel's hang guard raises a fault word in mapped host memory that the host
+    checks after every render whatever "verify" says: with the test option that raises
+    it, a synchronous render fails, a render_device with verify on fails, and one with verify off
+    returns and reports it at akr_hip_synchronize.  Renders after that succeed again."""
+    torch = pytest.importorskip("torch")
+    with hip_ctx_factory(0) as ctx:
+        cs, orc = _setup(ctx, cornell((32, 32)))
+        ctx.set_option("path", 1)
+        ctx.set_option("path_defer", 1)
+        tiles = [(0, 0, 32, 32)]
+        ctx.set_option("fault_test", 1)
+        with pytest.raises(capi.AkrError, match="hang guard"):
+            ctx.render(2, 5, tiles, 32, 32)
+        rad = torch.zeros(1024 * 3, device="cuda:0")
+        wt = torch.zeros(1024, device="cuda:0")
+        with pytest.raises(capi.AkrError, match="hang guard"):
+            ctx.render_device(2, 5, tiles, rad.data_ptr(), wt.data_ptr())
+        ctx.set_option("verify", 0)
+        ctx.render_device(2, 5, tiles, rad.data_ptr(), wt.data_ptr())
+        with pytest.raises(capi.AkrError, match="hang guard"):
+            ctx.synchronize()
+        ctx.set_option("verify", 1)
+        ctx.set_option("fault_test", 0)
+        _check_render(ctx, orc, 2, 5, tiles, 32, 32)
+
+
 def test_render_device_packed(hip_ctx_factory):
     torch = pytest.importorskip("torch")
     with hip_ctx_factory(0) as ctx:
