@@ -204,7 +204,14 @@ const char *akr_hip_last_error(const akr_hip_ctx *ctx);
  * "exact_cull", "wide", "lean", "shadow_grid_pct", "rays_per_lane" (tuning / A-B),
  * "lookahead" (speculative sample lanes per pixel, DESIGN.md §3.7: 1 = off (default), 0 = on
  * whenever "slot_target" gives a pixel two or more lanes, 2..64 = on with at most that many lanes;
- * results are identical for every value), "slot_target" (lookahead path slots per pass). */
+ * results are identical for every value), "slot_target" (lookahead path slots per pass).
+ * Render forms and their tuning (all give the same bits): "path" (0 wavefront,
+ * 1 persistent kernel, 2 auto), "path_defer", "path_defer_pixels", "path_auto_pixels",
+ * "path_auto_complex", "path_tab", "path_mix", "path_order", "path_order_min_spp",
+ * "path_order_shift", "path_order_pair", "path_prio", "path_min_wait", "path_grid_pct".
+ * "verify" (default 1): in-band film check after every render.  Test only: "pixel_probe" (record
+ * akr_pixel_probe per slot), "fault_test" (raise the hang guard's fault word once), "ray_steps",
+ * "serial_shadow", "any_far_first", "la_early_exit". */
 int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value);
 
 int akr_hip_upload_mesh(akr_hip_ctx *ctx, const float *vertices, uint64_t n_vertices,
