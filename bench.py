@@ -280,8 +280,10 @@ def main():
     t_gen = time.time() - t0
     ctx = capi.HipContext(local)
     t_setup = time.perf_counter()
+    # host BVH build threads: the job's usable CPUs shared by the ranks of this node (16 at most)
+    build_threads = max(2, min(16, host_cpus()["usable"] // max(1, world)))
     info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect, n_bins=args.bins,
-                              n_threads=min(16, os.cpu_count() or 1),
+                              n_threads=build_threads,
                               builder={"sah": capi.BUILDER_SAH, "lbvh": capi.BUILDER_LBVH,
                                        "sbvh": capi.BUILDER_SBVH}[args.builder],
                               spatial_budget=args.spatial_budget)
@@ -507,7 +509,7 @@ def main():
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                     for k, v in bstats.items()},
         "bvh": {"nodes": info.n_nodes, "depth": info.max_depth, "build_s": round(info.build_ms / 1e3, 2),
-                "setup_s": round(t_setup, 2)},
+                "setup_s": round(t_setup, 2), "build_threads": build_threads},
     }
     print(json.dumps(line), flush=True)
     if world > 1:
