@@ -125,6 +125,8 @@ EXPORTS = {
     "akr_hip_upload_materials": (C.c_int, [_P, _P, C.c_int32]),
     "akr_hip_upload_lights": (C.c_int, [_P, _P, C.c_int32, _P]),
     "akr_hip_build_accel": (C.c_int, [_P, C.POINTER(BuildParams)]),
+    "akr_hip_import_accel": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.c_int32]),
+    "akr_bvh_validate": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.c_uint64, C.POINTER(C.c_int32)]),
     "akr_hip_accel_info": (C.c_int, [_P, C.POINTER(AccelInfo)]),
     "akr_hip_accel_export": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64]),
     "akr_hip_set_camera": (C.c_int, [_P, C.POINTER(Camera)]),
@@ -216,6 +218,17 @@ def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost
     if wide:
         return nodes, tris, info, (wn, lv, root.value)
     return nodes, tris, info
+
+
+def validate_bvh(nodes, tris, n_scene_tris):
+    """Host check of a BVH2 (akr_bvh_validate): returns its depth, raises AkrError when malformed."""
+    nodes = np.ascontiguousarray(nodes, NODE_DTYPE)
+    tris = np.ascontiguousarray(tris, TRI_DTYPE)
+    d = C.c_int32(0)
+    if load_library().akr_bvh_validate(_ptr(nodes), nodes.shape[0], _ptr(tris), tris.shape[0], int(n_scene_tris),
+                                       C.byref(d)) != 0:
+        raise AkrError("malformed BVH")
+    return d.value
 
 
 def render_node(ctxs, spp, max_depth, tiles, width, height, ray_clamp=0.0, exact_cull=False, radiance=None,
@@ -324,6 +337,14 @@ class HipContext:
         (host SBVH with the reference's spatial splits; spatial_budget = extra references / triangles)."""
         p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget)
         self._check(self.lib.akr_hip_build_accel(self.h, C.byref(p)))
+        return self.accel_info()
+
+    def import_accel(self, nodes, tris, n_threads=0):
+        """Adopt a BVH2 exported by another context (accel_export) instead of building one."""
+        nodes = np.ascontiguousarray(nodes, NODE_DTYPE)
+        tris = np.ascontiguousarray(tris, TRI_DTYPE)
+        self._check(self.lib.akr_hip_import_accel(self.h, _ptr(nodes), nodes.shape[0], _ptr(tris), tris.shape[0],
+                                                  int(n_threads)))
         return self.accel_info()
 
     def accel_info(self) -> AccelInfo:

@@ -302,8 +302,10 @@ def _light_power(mesh: Mesh, prim: int, m: EmissiveMaterial) -> np.float32:
     return F32(float(area) * tc_area * float(I))
 
 
-def upload_scene(ctx: "capi.HipContext", cs: CompiledScene, build: bool = True, **build_kw):
-    """Upload a compiled scene through the C-ABI (the HipAccelerator adapter's commit)."""
+def upload_scene(ctx: "capi.HipContext", cs: CompiledScene, build: bool = True, bvh=None, **build_kw):
+    """Upload a compiled scene through the C-ABI (the HipAccelerator adapter's commit).  With
+    `bvh` = (nodes, tris) from another context's accel_export, that tree is adopted instead of
+    building one (n_threads from build_kw is kept for the wide view)."""
     ctx.upload_images(cs.images)
     ctx.upload_textures(cs.textures)
     ctx.upload_materials(cs.materials)
@@ -314,6 +316,8 @@ def upload_scene(ctx: "capi.HipContext", cs: CompiledScene, build: bool = True, 
     ctx.upload_lights(cs.lights, cs.power)
     cam = cs.camera
     ctx.set_camera(cam.position, cam.rotation, cam.fov, cam.resolution)
+    if bvh is not None:
+        return ctx.import_accel(bvh[0], bvh[1], n_threads=build_kw.get("n_threads", 0))
     if build:
         return ctx.build_accel(**build_kw)
     return None

@@ -84,6 +84,14 @@ struct Bvh4Output {
 // n_threads <= 0: one per hardware thread (at most 64).
 void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads = 0);
 
+// Checks a BVH2 handed in from outside (akr_hip_import_accel) before the library adopts it: node 0 is
+// the virtual root (child[1] EMPTY), every internal reference is < n_nodes and reached once from
+// the root (a tree), every leaf's triangle range lies inside `tris` with 1..AKR_LEAF_MAX triangles,
+// split axes are 0..2, boxes are not NaN, the depth is <= AKR_BVH_MAX_DEPTH and every triangle id
+// is < n_scene_tris.  Returns the depth (and the largest leaf in max_leaf); throws on violation.
+int validate_bvh2(const akr_bvh_node *nodes, uint64_t n_nodes, const akr_bvh_tri *tris, uint64_t n_tris,
+                  uint64_t n_scene_tris, int &max_leaf);
+
 // Outward 8-bit quantization of one bound (exposed for tests): the q with fmaf(q, s, origin) on
 // the correct side of `bound`, s = 2^(e - 127).
 uint32_t quantize_lo(float bound, float origin, float s);

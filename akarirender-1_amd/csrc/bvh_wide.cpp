@@ -275,6 +275,50 @@ uint32_t quantize_hi(float bound, float origin, float s) {
     return qi;
 }
 
+int validate_bvh2(const akr_bvh_node *nodes, uint64_t n_nodes, const akr_bvh_tri *tris, uint64_t n_tris,
+                  uint64_t n_scene_tris, int &max_leaf) {
+    max_leaf = 0;
+    if (n_nodes == 0) throw std::runtime_error("BVH: no nodes");
+    if (n_nodes >= AKR_CHILD_LEAF) throw std::runtime_error("BVH: too many nodes");
+    if (nodes[0].child[1] != AKR_CHILD_EMPTY) throw std::runtime_error("BVH: node 0 is not the virtual root");
+    for (uint64_t t = 0; t < n_tris; t++)
+        if (tris[t].gid >= n_scene_tris) throw std::runtime_error("BVH: triangle id beyond the scene");
+    std::vector<uint8_t> seen(n_nodes, 0);
+    std::vector<std::pair<uint32_t, int>> st;  // (node, depth)
+    int depth = 0;
+    auto child = [&](uint32_t r, int d) {
+        if (r == AKR_CHILD_EMPTY) return;
+        if (r & AKR_CHILD_LEAF) {
+            const uint64_t first = akr_leaf_first(r), cnt = akr_leaf_count(r);
+            if (cnt > AKR_LEAF_MAX || first + cnt > n_tris) throw std::runtime_error("BVH: leaf outside the triangles");
+            max_leaf = std::max(max_leaf, (int)cnt);
+            depth = std::max(depth, d);
+            return;
+        }
+        if (r == 0 || r >= n_nodes) throw std::runtime_error("BVH: node reference out of range");
+        if (seen[r]) throw std::runtime_error("BVH: a node is reached twice (not a tree)");
+        seen[r] = 1;
+        st.push_back({r, d});
+    };
+    seen[0] = 1;
+    child(nodes[0].child[0], 1);
+    while (!st.empty()) {
+        const auto [n, d] = st.back();
+        st.pop_back();
+        if (d > AKR_BVH_MAX_DEPTH) throw std::runtime_error("BVH: deeper than AKR_BVH_MAX_DEPTH");
+        depth = std::max(depth, d);
+        const akr_bvh_node &x = nodes[n];
+        if (x.axis > 2) throw std::runtime_error("BVH: split axis out of range");
+        const float *v[3] = {x.bxy0, x.bxy1, x.bz};
+        for (int a = 0; a < 3; a++)
+            for (int k = 0; k < 4; k++)
+                if (std::isnan(v[a][k])) throw std::runtime_error("BVH: NaN in a node box");
+        child(x.child[0], d + 1);
+        child(x.child[1], d + 1);
+    }
+    return depth;
+}
+
 void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads) {
     out.nodes.clear();
     out.leaves.clear();

@@ -1358,20 +1358,12 @@ int akr_hip_upload_lights(akr_hip_ctx *ctx, const akr_area_light *lights, int32_
     });
 }
 
-int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
-    return guard(ctx, [&] {
-        akr_build_params p{};
-        p.max_leaf_size = 4;
-        p.n_bins = 32;
-        p.traversal_cost = 1.0f;
-        p.intersect_cost = 4.0f;
-        if (params) p = *params;
-        BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
-        if (p.builder == AKR_BUILDER_LBVH) build_lbvh_gpu(in, ctx->bvh, ctx->stream);
-        else if (p.builder == AKR_BUILDER_SAH || p.builder == AKR_BUILDER_SBVH) build_bvh(in, p, ctx->bvh);
-        else throw std::runtime_error("unknown builder");
+namespace {
+// After the BVH2 of ctx->bvh exists (built or imported): the wide view, its device copy, the BVH2
+// itself for the exact lane path, the accel info, and the scene's shading records.
+void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         auto &b = ctx->bvh;
-        build_bvh4(b.nodes, ctx->bvh4, p.n_threads);
+        build_bvh4(b.nodes, ctx->bvh4, n_threads);
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
         // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
         // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the
@@ -1393,7 +1385,7 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         auto remap = [&](uint32_t r) {
             return (r != AKR_CHILD_EMPTY && (r & AKR_CHILD_LEAF)) ? (AKR_CHILD_LEAF | leaf_off[r & 0x7FFFFFFFu]) : r;
         };
-        const int nt = p.n_threads > 0 ? std::min(p.n_threads, 64)
+        const int nt = n_threads > 0 ? std::min(n_threads, 64)
                                        : (int)std::min(64u, std::max(1u, std::thread::hardware_concurrency()));
         auto fill = [&](int t) {
             const size_t l0 = leaves.size() * t / nt, l1 = leaves.size() * (t + 1) / nt;
@@ -1431,6 +1423,41 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         ctx->info.sah_cost = b.sah_cost;
         ctx->accel_built = true;
         ctx->commit_scene();
+}
+}  // namespace
+
+int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
+    return guard(ctx, [&] {
+        akr_build_params p{};
+        p.max_leaf_size = 4;
+        p.n_bins = 32;
+        p.traversal_cost = 1.0f;
+        p.intersect_cost = 4.0f;
+        if (params) p = *params;
+        BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
+        if (p.builder == AKR_BUILDER_LBVH) build_lbvh_gpu(in, ctx->bvh, ctx->stream);
+        else if (p.builder == AKR_BUILDER_SAH || p.builder == AKR_BUILDER_SBVH) build_bvh(in, p, ctx->bvh);
+        else throw std::runtime_error("unknown builder");
+        finish_accel(ctx, p.n_threads);
+    });
+}
+
+int akr_hip_import_accel(akr_hip_ctx *ctx, const void *nodes, uint64_t n_nodes, const void *tris, uint64_t n_tris,
+                         int32_t n_threads) {
+    return guard(ctx, [&] {
+        if (!nodes || n_nodes == 0 || (n_tris && !tris)) throw std::runtime_error("null or empty BVH arrays");
+        const auto *nd = reinterpret_cast<const akr_bvh_node *>(nodes);
+        const auto *tr = reinterpret_cast<const akr_bvh_tri *>(tris);
+        int max_leaf = 0;
+        const int depth = validate_bvh2(nd, n_nodes, tr, n_tris, ctx->n_tris(), max_leaf);  // throws on bad input
+        BvhOutput &b = ctx->bvh;
+        b.nodes.assign(nd, nd + n_nodes);
+        b.tris.assign(tr, tr + n_tris);
+        b.max_depth = depth;
+        b.max_leaf = max_leaf;
+        b.sah_cost = 0.0;  // not known for an imported tree
+        b.build_ms = 0.0;
+        finish_accel(ctx, n_threads);
     });
 }
 
@@ -1731,6 +1758,20 @@ int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t
 const void *akr_bvh_host_nodes(const akr_bvh_host *h) { return h ? h->out.nodes.data() : nullptr; }
 const void *akr_bvh_host_tris(const akr_bvh_host *h) { return h ? h->out.tris.data() : nullptr; }
 void akr_bvh_host_free(akr_bvh_host *h) { delete h; }
+
+int akr_bvh_validate(const void *nodes, uint64_t n_nodes, const void *tris, uint64_t n_tris, uint64_t n_scene_tris,
+                     int32_t *max_depth) {
+    try {
+        if (!nodes || (n_tris && !tris)) return -1;
+        int max_leaf = 0;
+        const int d = validate_bvh2(reinterpret_cast<const akr_bvh_node *>(nodes), n_nodes,
+                                    reinterpret_cast<const akr_bvh_tri *>(tris), n_tris, n_scene_tris, max_leaf);
+        if (max_depth) *max_depth = d;
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
 
 int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, uint32_t *root_ref) {
     if (!h) return -1;

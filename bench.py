@@ -167,6 +167,34 @@ def spawn_ranks(n: int, argv, need_devices: bool = True) -> int:
     return subprocess.run(cmd).returncode
 
 
+def build_once_per_node(rank: int, build, export, adopt, barrier, tag: str, shm_dir: Path = Path("/dev/shm")):
+    """Rank 0 runs `build()` and leaves the BVH2 that `export()` returns in shared memory (one .npy
+    per array, written under a temporary name and renamed); after a barrier the other ranks map the
+    files and run `adopt(nodes, tris)`; after a second barrier rank 0 removes them.  Returns what
+    build / adopt returned."""
+    base = shm_dir / f"akr_bench_bvh_{tag}"
+    path = lambda name: Path(f"{base}_{name}.npy")
+    info = None
+    if rank == 0:
+        info = build()
+        nodes, tris = export()
+        for name, a in (("nodes", nodes), ("tris", tris)):
+            tmp = Path(f"{base}_{name}.tmp.npy")
+            np.save(tmp, a)
+            os.replace(tmp, path(name))
+        del nodes, tris
+    barrier()
+    try:
+        if rank != 0:
+            info = adopt(np.load(path("nodes"), mmap_mode="r"), np.load(path("tris"), mmap_mode="r"))
+    finally:
+        barrier()
+        if rank == 0:
+            for name in ("nodes", "tris"):
+                path(name).unlink(missing_ok=True)
+    return info
+
+
 def launch_check(world: int, rank: int):
     """--launch-check: the rank plumbing without a GPU (gloo): every rank joins the group and
     all-gathers a packed film the size of its tile share; rank 0 prints the live world size."""
@@ -282,12 +310,21 @@ def main():
     t_setup = time.perf_counter()
     # host BVH build threads: the job's usable CPUs shared by the ranks of this node (16 at most)
     build_threads = max(2, min(16, host_cpus()["usable"] // max(1, world)))
-    info = scene.upload_scene(ctx, cs, max_leaf_size=args.leaf, intersect_cost=args.sah_isect, n_bins=args.bins,
-                              n_threads=build_threads,
-                              builder={"sah": capi.BUILDER_SAH, "lbvh": capi.BUILDER_LBVH,
-                                       "sbvh": capi.BUILDER_SBVH}[args.builder],
-                              spatial_budget=args.spatial_budget)
-    t_setup = time.perf_counter() - t_setup  # BVH2 build + wide collapse + upload
+    build_kw = dict(max_leaf_size=args.leaf, intersect_cost=args.sah_isect, n_bins=args.bins, n_threads=build_threads,
+                    builder={"sah": capi.BUILDER_SAH, "lbvh": capi.BUILDER_LBVH, "sbvh": capi.BUILDER_SBVH}[args.builder],
+                    spatial_budget=args.spatial_budget)
+    if world > 1:
+        # the node's ranks build the scene's BVH once (8 concurrent 10M-triangle SBVH builds would share
+        # the host's CPUs): rank 0 builds it, the others adopt its BVH2 (akr_hip_import_accel:
+        # validated, bit-identical results)
+        full_kw = dict(build_kw, n_threads=max(2, min(16, host_cpus()["usable"])))
+        info = build_once_per_node(
+            rank, build=lambda: scene.upload_scene(ctx, cs, **full_kw), export=ctx.accel_export,
+            adopt=lambda nodes, tris: scene.upload_scene(ctx, cs, bvh=(nodes, tris), n_threads=build_threads),
+            barrier=dist.barrier, tag=os.environ.get("MASTER_PORT", "0"))
+    else:
+        info = scene.upload_scene(ctx, cs, **build_kw)
+    t_setup = time.perf_counter() - t_setup  # BVH2 build (or import) + wide collapse + upload
     if args.rays_per_lane != 1:
         ctx.set_option("rays_per_lane", args.rays_per_lane)
     ctx.set_option("wide", args.wide)

@@ -225,6 +225,12 @@ int akr_hip_upload_materials(akr_hip_ctx *ctx, const akr_material *materials, in
 int akr_hip_upload_lights(akr_hip_ctx *ctx, const akr_area_light *lights, int32_t n,
                           const float *power);
 int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params);
+/* Adopt a BVH2 built elsewhere (the arrays akr_hip_accel_export writes: akr_bvh_node[n_nodes],
+ * akr_bvh_tri[n_tris]) for the uploaded meshes, instead of building one: the same wide view and
+ * device copy follow.  The tree is validated first (akr_bvh_validate); results are those of the
+ * context that built it, bit for bit.  Lets the ranks of a node build the scene's BVH once. */
+int akr_hip_import_accel(akr_hip_ctx *ctx, const void *nodes, uint64_t n_nodes, const void *tris,
+                         uint64_t n_tris, int32_t n_threads);
 int akr_hip_accel_info(akr_hip_ctx *ctx, akr_accel_info *info);
 int akr_hip_accel_export(akr_hip_ctx *ctx, void *nodes, uint64_t node_bytes, void *tris,
                          uint64_t tri_bytes);
@@ -282,6 +288,10 @@ void akr_bvh_host_free(akr_bvh_host *h);
 /* The 4-wide quantized view the traversal kernels walk (akr_bvh4_node / akr_bvh_leaf), built from
  * the handle's BVH2 on first call; pointers stay valid until akr_bvh_host_free. */
 int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, uint32_t *root_ref);
+/* Host check of a BVH2 before it is adopted (no device): a tree from the virtual root, references and
+ * leaf ranges in range, triangle ids < n_scene_tris, depth <= AKR_BVH_MAX_DEPTH.  0 = valid. */
+int akr_bvh_validate(const void *nodes, uint64_t n_nodes, const void *tris, uint64_t n_tris,
+                     uint64_t n_scene_tris, int32_t *max_depth);
 const void *akr_bvh_host_wide_nodes(const akr_bvh_host *h);
 const void *akr_bvh_host_wide_leaves(const akr_bvh_host *h);
 

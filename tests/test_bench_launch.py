@@ -2,6 +2,7 @@
 torch.distributed.run; under a launcher --gpus must equal WORLD_SIZE; the JSON line's n_gpus is the
 live group's size.  Rehearsed on CPU with gloo (--launch-check: rank plumbing + frame-end gather)."""
 import json
+from pathlib import Path
 import subprocess
 import sys
 
@@ -95,3 +96,39 @@ print("LAUNCHER-CLEAN")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env,
                        cwd=str(ROOT))
     assert r.returncode == 0 and "LAUNCHER-CLEAN" in r.stdout, r.stderr[-3000:]
+
+
+def _share_worker(rank, world, port, shm_dir, out_dir):
+    import os as _os
+    import torch.distributed as dist
+    import numpy as _np
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, str(ROOT))
+    import bench as b
+    from akari_amd import capi
+    nodes = _np.zeros(5, capi.NODE_DTYPE)
+    nodes["axis"] = _np.arange(5)
+    tris = _np.zeros(3, capi.TRI_DTYPE)
+    tris["gid"] = [7, 8, 9]
+    calls = []
+    info = b.build_once_per_node(rank, build=lambda: calls.append("build") or "built", export=lambda: (nodes, tris),
+                                 adopt=lambda n, t: calls.append("adopt") or (n.tobytes() == nodes.tobytes() and
+                                                                              t.tobytes() == tris.tobytes()),
+                                 barrier=dist.barrier, tag="t", shm_dir=Path(shm_dir))
+    dist.barrier()
+    Path(out_dir, f"r{rank}").write_text(f"{info}|{','.join(calls)}")
+    dist.destroy_process_group()
+
+
+def test_bvh_built_once_per_node(tmp_path):
+    """bench.py's multi-rank setup: rank 0 builds and shares the BVH2 through shared-memory files,
+    the other ranks adopt an identical copy, and the files are removed afterwards (gloo, 3 ranks)."""
+    import torch.multiprocessing as mp
+    shm, out = tmp_path / "shm", tmp_path / "out"
+    shm.mkdir()
+    out.mkdir()
+    mp.spawn(_share_worker, args=(3, bench._free_port(), str(shm), str(out)), nprocs=3, join=True)
+    assert (out / "r0").read_text() == "built|build"
+    assert (out / "r1").read_text() == (out / "r2").read_text() == "True|adopt"
+    assert list(shm.iterdir()) == []

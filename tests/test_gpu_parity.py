@@ -343,6 +343,29 @@ def test_render_node_overlapping_tiles_prefilled(hip_ctx_factory):
             capi.render_node([a, b, a], 3, 5, tiles, 40, 24)
 
 
+def test_import_accel_bit_exact(hip_ctx_factory):
+    """akr_hip_import_accel: a context that adopts another context's exported BVH2 (the ranks of a
+    node build once, bench.py) traces and renders bit for bit like the context that built it, and a
+    malformed tree is refused with a status, not adopted."""
+    sc = small_soup(100_000, (64, 36))
+    with hip_ctx_factory(0) as a, hip_ctx_factory(0) as b:
+        cs, orc = _setup(a, sc, builder=capi.BUILDER_SBVH, n_threads=8)
+        nodes, tris = a.accel_export()
+        info = scene.upload_scene(b, cs, bvh=(nodes, tris), n_threads=8)
+        ia = a.accel_info()
+        assert (info.n_nodes, info.n_tris, info.max_depth, info.max_leaf) == (ia.n_nodes, ia.n_tris, ia.max_depth,
+                                                                              ia.max_leaf)
+        rays = random_rays(1 << 14, 77, -1.0, 1.0)
+        for any_hit in (False, True):
+            ha, hb = a.trace(rays, any_hit), b.trace(rays, any_hit)
+            assert ha.tobytes() == hb.tobytes()
+        _check_render(b, orc, 3, 5, [(0, 0, 64, 36)], 64, 36)
+        bad = nodes.copy()
+        bad[3]["child"][0] = len(nodes) + 10
+        with pytest.raises(capi.AkrError, match="BVH"):
+            b.import_accel(bad, tris)
+
+
 def test_hang_guard_fault_is_reported(hip_ctx_factory):
     """The persistent kernel's hang guard raises a fault word in mapped host memory that the host
     checks after every render whatever "verify" says: with the test option that raises

@@ -139,6 +139,52 @@ def test_wide_view_invariants(leaf, builder):
                     assert np.all(lo <= lv[i]["lo"]) and np.all(hi >= lv[i]["hi"])
 
 
+def test_bvh_validate_accepts_built_trees_and_rejects_malformed_ones():
+    """akr_bvh_validate, the check akr_hip_import_accel runs before it adopts a foreign BVH2: every
+    tree the builders make passes with its depth; a reference out of range, a node reached twice
+    (a cycle or a DAG), a leaf beyond the triangles, a triangle id beyond the scene, a bad split axis,
+    a NaN box, a node 0 that is not the virtual root or an over-deep chain are rejected."""
+    cs = scene.compile_scene(small_soup(3_000))
+    for b in (capi.BUILDER_SAH, capi.BUILDER_SBVH):
+        nodes, tris, info = capi.build_bvh_host(cs.vertices, cs.indices, builder=b)
+        assert capi.validate_bvh(nodes, tris, cs.n_tris) == info.max_depth
+    nodes, tris, info = capi.build_bvh_host(cs.vertices, cs.indices)
+    internal = [i for i in range(1, len(nodes)) if not (int(nodes[i]["child"][0]) & 0x80000000)]
+    k = internal[len(internal) // 2]
+
+    def bad(mut_nodes=None, mut_tris=None, n_scene=cs.n_tris):
+        n, t = nodes.copy(), tris.copy()
+        if mut_nodes:
+            mut_nodes(n)
+        if mut_tris:
+            mut_tris(t)
+        with pytest.raises(capi.AkrError):
+            capi.validate_bvh(n, t, n_scene)
+
+    bad(lambda n: n[k]["child"].__setitem__(0, len(nodes) + 5))                    # out of range
+    bad(lambda n: n[k]["child"].__setitem__(0, int(n[0]["child"][0])))             # back to the root: a cycle
+    bad(lambda n: n[k]["child"].__setitem__(0, 0))                                  # the virtual root
+    bad(lambda n: n[k]["child"].__setitem__(1, 0x80000000 | (len(tris) << 3) | 3))  # leaf beyond the triangles
+    bad(mut_tris=lambda t: t["gid"].__setitem__(7, cs.n_tris))                      # triangle id beyond the scene
+    bad(lambda n: n[k].__setitem__("axis", 3))
+    bad(lambda n: n[k]["bz"].__setitem__(1, np.nan))
+    bad(lambda n: n[0]["child"].__setitem__(1, 1))                                  # node 0 not the virtual root
+    bad(n_scene=0)
+    # a chain deeper than AKR_BVH_MAX_DEPTH (64): node i -> node i + 1, the other child a leaf
+    deep = np.zeros(70, capi.NODE_DTYPE)
+    deep["child"][:, 1] = 0x80000000
+    for i in range(1, 69):
+        deep[i]["child"][0] = i + 1
+    deep[0]["child"] = [1, 0xFFFFFFFF]
+    deep[69]["child"] = [0x80000000, 0x80000000]
+    deep["axis"] = 0
+    with pytest.raises(capi.AkrError):
+        capi.validate_bvh(deep, tris[:1], cs.n_tris)
+    empty = np.zeros(1, capi.NODE_DTYPE)
+    empty[0]["child"] = [0xFFFFFFFF, 0xFFFFFFFF]
+    assert capi.validate_bvh(empty, tris[:0], 0) == 0
+
+
 @pytest.mark.parametrize("builder", ["sah", "sbvh"])
 def test_wide_view_preorder_parallel(builder):
     """Large enough that the collapse runs subtrees on the thread pool (bvh_wide.cpp: pending
