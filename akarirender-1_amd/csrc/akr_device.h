@@ -51,6 +51,7 @@ constexpr int kRefillMinAny = AKR_REFILL_MIN_ANY;  // the same for occlusion (an
 #ifndef AKR_WHILE_EXIT
 #define AKR_WHILE_EXIT 16
 #endif
+constexpr uint64_t kMaxWideNodes = 1ull << 26;  // 64-B wide nodes addressed by a 32-bit byte offset (visit_wide_lean)
 constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
 constexpr int kWhileExitAny = AKR_WHILE_EXIT_ANY;  // the same for occlusion traces
 #ifndef AKR_WORK_SHARDS

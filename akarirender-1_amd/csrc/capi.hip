@@ -1364,6 +1364,8 @@ namespace {
 void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         auto &b = ctx->bvh;
         build_bvh4(b.nodes, ctx->bvh4, n_threads);
+        if (ctx->bvh4.nodes.size() >= kMaxWideNodes)
+            throw std::runtime_error("scene too large: the wide view needs fewer than 2^26 nodes (about 100 M triangles)");
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
         // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
         // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the
