@@ -183,15 +183,16 @@ def build_once_per_node(rank: int, build, export, adopt, barrier, tag: str, shm_
             np.save(tmp, a)
             os.replace(tmp, path(name))
         del nodes, tris
-    barrier()
     try:
+        barrier()
         if rank != 0:
             info = adopt(np.load(path("nodes"), mmap_mode="r"), np.load(path("tris"), mmap_mode="r"))
-    finally:
         barrier()
+    finally:  # the files hold ~1.5 GB of host memory: rank 0 removes them however the others fared
         if rank == 0:
             for name in ("nodes", "tris"):
                 path(name).unlink(missing_ok=True)
+                Path(f"{base}_{name}.tmp.npy").unlink(missing_ok=True)
     return info
 
 
