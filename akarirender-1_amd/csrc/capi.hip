@@ -252,6 +252,10 @@ struct akr_hip_ctx {
     // whose lanes seldom have spare capacity)
     int path_defer = 2;
     int64_t path_defer_pixels = 600000;
+    // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
+    // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
+    // 0.300 ms; a 100K-triangle soup: 0.665 against 0.571 ms)
+    int64_t path_defer_min_tris = 10000;
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
     // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
@@ -919,7 +923,8 @@ struct akr_hip_ctx {
                 pa.fault = d_fault_host;
                 pa.fault_test = fault_test ? 1u : 0u;
                 const bool defer = p.max_depth <= 8 &&
-                                   (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels));
+                                   (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels &&
+                                                        (int64_t)n_tris() >= path_defer_min_tris));
                 // the shading's material / light / CDF tables in LDS when they fit
                 const bool tab = path_tab && path_tab_fits(n_mats, n_lights);
                 const uint64_t resident = (uint64_t)path_grid[defer][tab] * (uint64_t)path_grid_pct / 100;
@@ -1238,6 +1243,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_defer") {
             if (value < 0 || value > 2) throw std::runtime_error("path_defer must be 0, 1 or 2 (auto)");
             ctx->path_defer = (int)value;
+        } else if (k == "path_defer_min_tris") {
+            if (value < 0) throw std::runtime_error("path_defer_min_tris must be >= 0");
+            ctx->path_defer_min_tris = value;
         } else if (k == "path_defer_pixels") {
             if (value < 0) throw std::runtime_error("path_defer_pixels must be >= 0");
             ctx->path_defer_pixels = value;
