@@ -558,6 +558,15 @@ def test_auto_form_by_shading(hip_ctx_factory):
                 _check_render(ctx, orc, 3, 5, [(0, 0, 32, 32)], 32, 32)
                 want = "path" if (simple or complex_ok) else "trace_closest"
                 assert set(ctx.kernel_stats()) == {want}, (sc, complex_ok, ctx.kernel_stats())
+                # a 36-triangle scene takes k_path even at a small pixel count (path_defer_min_tris)
+                assert ctx.render_form()["form"] == ("k_path" if (simple or complex_ok) else "wavefront")
+    with hip_ctx_factory(0) as ctx:   # >= 10K triangles at <= 600K pixels: the deferred form
+        cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
+        _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
+        assert ctx.render_form()["form"] == "k_path_defer"
+        ctx.set_option("path_defer_min_tris", 10 ** 9)
+        _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
+        assert ctx.render_form()["form"] == "k_path"
 
 
 def _tab_fits(cs):
