@@ -274,6 +274,12 @@ struct akr_hip_ctx {
     int path_order_pair = 2;
     int path_prio = 0;
     int path_order_min_spp = 64;
+    // renders of at most path_order_share_pixels pixels (a rank's share of a 2-, 4- or 8-way split)
+    // take the order from path_order_share_min_spp samples: the pilot's cost shrinks with the pixel
+    // count and the launch tail it shortens does not (C3 at 20 spp, DESIGN.md §3.10: 2- / 4- / 8-way
+    // shares 1.5 / 4.5 / 3 % faster with the order, the whole frame unchanged)
+    int64_t path_order_share_pixels = 1200000;
+    int path_order_share_min_spp = 16;
     int path_order_shift = 2;
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -942,7 +948,10 @@ struct akr_hip_ctx {
                     pixel_order((uint32_t)std::min<uint64_t>(N, 64), ms);
                     order_warm = true;
                 }
-                if (path_order != 0 && (!defer || path_order == 2) && p.spp >= path_order_min_spp && N >= 2) {
+                const int order_min_spp = (int64_t)N <= path_order_share_pixels
+                                              ? std::min(path_order_share_min_spp, path_order_min_spp)
+                                              : path_order_min_spp;
+                if (path_order != 0 && (!defer || path_order == 2) && p.spp >= order_min_spp && N >= 2) {
                     timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
                     pa.order = d_oidx[1].p;
                     const bool pair = defer && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000));
@@ -1255,6 +1264,12 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_min_spp") {
             if (value < 0) throw std::runtime_error("path_order_min_spp must be >= 0");
             ctx->path_order_min_spp = (int)std::min<int64_t>(value, INT32_MAX);
+        } else if (k == "path_order_share_pixels") {
+            if (value < 0) throw std::runtime_error("path_order_share_pixels must be >= 0");
+            ctx->path_order_share_pixels = value;
+        } else if (k == "path_order_share_min_spp") {
+            if (value < 0) throw std::runtime_error("path_order_share_min_spp must be >= 0");
+            ctx->path_order_share_min_spp = (int)std::min<int64_t>(value, INT32_MAX);
         } else if (k == "path_order_shift") {
             if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
             ctx->path_order_shift = (int)value;

@@ -208,7 +208,7 @@ const char *akr_hip_last_error(const akr_hip_ctx *ctx);
  * Render forms and their tuning (all give the same bits): "path" (0 wavefront,
  * 1 persistent kernel, 2 auto), "path_defer", "path_defer_pixels", "path_defer_min_tris", "path_auto_pixels",
  * "path_auto_complex", "path_tab", "path_mix", "path_order", "path_order_min_spp",
- * "path_order_shift", "path_order_pair", "path_prio", "path_min_wait", "path_grid_pct".
+ * "path_order_share_pixels", "path_order_share_min_spp", "path_order_shift", "path_order_pair", "path_prio", "path_min_wait", "path_grid_pct".
  * "verify" (default 1): in-band film check after every render.  Test only: "pixel_probe" (record
  * akr_pixel_probe per slot), "fault_test" (raise the hang guard's fault word once), "ray_steps",
  * "serial_shadow", "any_far_first", "la_early_exit". */

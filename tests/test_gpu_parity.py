@@ -563,7 +563,13 @@ def test_auto_form_by_shading(hip_ctx_factory):
     with hip_ctx_factory(0) as ctx:   # >= 10K triangles at <= 600K pixels: the deferred form
         cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
         _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
-        assert ctx.render_form()["form"] == "k_path_defer"
+        assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
+        # a small render takes the cost-ordered fetch from path_order_share_min_spp (16) samples
+        _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
+        assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}
+        ctx.set_option("path_order_share_pixels", 1000)
+        _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
+        assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
         ctx.set_option("path_defer_min_tris", 10 ** 9)
         _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
         assert ctx.render_form()["form"] == "k_path"
