@@ -62,7 +62,7 @@ class Rect(C.Structure):
 class BuildParams(C.Structure):
     _fields_ = [("max_leaf_size", C.c_int32), ("n_bins", C.c_int32), ("traversal_cost", C.c_float),
                 ("intersect_cost", C.c_float), ("n_threads", C.c_int32), ("builder", C.c_int32),
-                ("spatial_budget", C.c_float), ("_pad", C.c_int32)]
+                ("spatial_budget", C.c_float), ("wide_collapse", C.c_int32)]
 
 
 class AccelInfo(C.Structure):
@@ -88,6 +88,7 @@ class PixelProbe(C.Structure):
 TEX_CONSTANT, TEX_IMAGE = 0, 1
 PT_EXACT_CULL = 1
 BUILDER_SAH, BUILDER_LBVH, BUILDER_SBVH = 0, 1, 2
+COLLAPSE_SAH, COLLAPSE_BALANCED = 0, 1   # akr_build_params::wide_collapse
 MAT_DIFFUSE, MAT_GLOSSY, MAT_EMISSIVE, MAT_MIX = 0, 1, 2, 3
 PROBE_SEED, PROBE_RAYS = 1, 2
 FORM_NAMES = {-1: None, 0: "wavefront", 1: "wavefront+lookahead", 2: "k_path", 3: "k_path_defer"}
@@ -101,7 +102,7 @@ NODE_DTYPE = np.dtype([("bxy0", np.float32, 4), ("bxy1", np.float32, 4), ("bz", 
 TRI_DTYPE = np.dtype([("v0", np.float32, 3), ("gid", np.uint32), ("e1", np.float32, 3), ("_p0", np.uint32),
                       ("e2", np.float32, 3), ("_p1", np.uint32)])
 NODE4_DTYPE = np.dtype([("origin", np.float32, 3), ("meta", np.uint32), ("child", np.uint32, 4),
-                        ("q", np.uint32, 6), ("_pad", np.uint32, 2)])
+                        ("q", np.uint32, 6), ("order", np.uint32, 2)])
 PROBE_DTYPE = np.dtype([("seed", np.uint32), ("closest_rays", np.uint32), ("shadow_rays", np.uint32),
                         ("flags", np.uint32)])
 LEAF_DTYPE = np.dtype([("lo", np.float32, 3), ("hi", np.float32, 3), ("first", np.uint32), ("count", np.uint32)])
@@ -184,14 +185,16 @@ def device_count() -> int:
 
 
 def build_bvh_host(vertices, indices, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0,
-                   n_threads=0, wide=False, builder=0, spatial_budget=0.0):
+                   n_threads=0, wide=False, builder=0, spatial_budget=0.0, wide_collapse=0):
     """Run the product BVH builder on the host (no device): returns (nodes, tris, info), plus
-    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide`.  builder: BUILDER_SAH
+    (wide_nodes, leaves, root_ref) of the 4-wide traversal view when `wide` (wide_collapse:
+    COLLAPSE_SAH or COLLAPSE_BALANCED).  builder: BUILDER_SAH
     or BUILDER_SBVH (the host builders)."""
     lib = load_library()
     v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
     i = np.ascontiguousarray(indices, np.int32).reshape(-1)
-    p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget)
+    p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget,
+                    wide_collapse)
     h = C.c_void_p()
     info = AccelInfo()
     st = lib.akr_bvh_host_build(_ptr(v), v.size // 3, _ptr(i), i.size // 3, C.byref(p), C.byref(h), C.byref(info))
@@ -332,10 +335,12 @@ class HipContext:
         self._check(self.lib.akr_hip_upload_lights(self.h, C.cast(arr, C.c_void_p), len(lights), _ptr(pw)))
 
     def build_accel(self, max_leaf_size=4, n_bins=32, traversal_cost=1.0, intersect_cost=4.0, n_threads=0,
-                    builder=0, spatial_budget=0.0):
+                    builder=0, spatial_budget=0.0, wide_collapse=0):
         """builder: BUILDER_SAH (host binned SAH), BUILDER_LBVH (GPU Morton / Karras) or BUILDER_SBVH
-        (host SBVH with the reference's spatial splits; spatial_budget = extra references / triangles)."""
-        p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget)
+        (host SBVH with the reference's spatial splits; spatial_budget = extra references / triangles).
+        wide_collapse: COLLAPSE_SAH (default) or COLLAPSE_BALANCED, the traversal's 4-wide view."""
+        p = BuildParams(max_leaf_size, n_bins, traversal_cost, intersect_cost, n_threads, builder, spatial_budget,
+                    wide_collapse)
         self._check(self.lib.akr_hip_build_accel(self.h, C.byref(p)))
         return self.accel_info()
 

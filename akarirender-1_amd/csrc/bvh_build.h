@@ -81,8 +81,9 @@ struct Bvh4Output {
     float max_abs = 0.0f;  // largest |frame origin| and frame step 2^e over all wide nodes (lean test bound)
 };
 
-// n_threads <= 0: one per hardware thread (at most 64).
-void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads = 0);
+// n_threads <= 0: one per hardware thread (at most 64).  collapse: AKR_COLLAPSE_SAH (default) or
+// AKR_COLLAPSE_BALANCED (akr_hip.h; bvh_wide.cpp gather_slots).
+void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads = 0, int collapse = 0);
 
 // Checks a BVH2 handed in from outside (akr_hip_import_accel) before the library adopts it: node 0 is
 // the virtual root (child[1] EMPTY), every internal reference is < n_nodes and reached once from

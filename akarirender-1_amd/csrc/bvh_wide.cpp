@@ -52,30 +52,83 @@ Box child_box(const akr_bvh_node &n, int c) {
     return b;
 }
 
-// Slots of the wide node for BVH2 internal node `n`: its children, with internal children
-// replaced by their two children.
-int gather_slots(const std::vector<akr_bvh_node> &in, uint32_t n2, uint32_t slot_ref2[4], Box slot_box[4],
-                 uint32_t axis[3]) {
-    const akr_bvh_node &n = in[n2];
-    for (int s = 0; s < 4; s++) slot_ref2[s] = AKR_CHILD_EMPTY;
-    axis[0] = n.axis;
-    axis[1] = axis[2] = 0;
-    for (int c = 0; c < 2; c++) {
-        const uint32_t r = n.child[c];
-        if (r == AKR_CHILD_EMPTY) continue;
-        if (r & AKR_CHILD_LEAF) {
-            slot_ref2[2 * c] = r;
-            slot_box[2 * c] = child_box(n, c);
-        } else {
-            const akr_bvh_node &m = in[r];
-            axis[1 + c] = m.axis;
-            for (int g = 0; g < 2; g++) {
-                slot_ref2[2 * c + g] = m.child[g];
-                slot_box[2 * c + g] = child_box(m, g);
-            }
+// Slots of the wide node for BVH2 internal node `n`: a treelet of at most three BVH2 internal nodes
+// (n and up to two nodes below it) whose at most four frontier children are the slots.  `code`
+// names the treelet (n with children a, b; a0, a1 the children of a):
+//   0 {n}, 1 {n, a}, 2 {n, b}, 3 {n, a, b}, 4 {n, a, a0}, 5 {n, a, a1}, 6 {n, b, b0}, 7 {n, b, b1}
+// (Collapser::choose picks it).  Slots are stored in the treelet's depth-first order with no flips;
+// order[0..1] hold, per ray direction octant o (bit a = d[a] > 0), the slot permutation of the BVH2
+// depth-first order: byte o of the pair, two bits per slot = that slot's position (near = left iff
+// d[axis] > 0 at each node).
+int gather_slots(const std::vector<akr_bvh_node> &in, uint32_t n2, int code, uint32_t slot_ref2[4], Box slot_box[4],
+                 uint32_t order[2]) {
+    struct TN {
+        uint32_t ref;  // BVH2 reference of a frontier entry (leaf, EMPTY or an unopened node)
+        Box box;
+        int kid[2];    // opened: treelet indices of its children; -1 while a frontier entry
+        uint32_t axis;
+    };
+    TN tn[7];
+    int n_tn = 1;
+    tn[0].ref = n2;
+    auto open = [&](int i) {
+        const akr_bvh_node &m = in[tn[i].ref];
+        tn[i].axis = m.axis;
+        for (int c = 0; c < 2; c++) {
+            tn[n_tn].ref = m.child[c];
+            tn[n_tn].box = child_box(m, c);
+            tn[n_tn].kid[0] = tn[n_tn].kid[1] = -1;
+            tn[i].kid[c] = n_tn++;
         }
+    };
+    open(0);  // tn[1] = a, tn[2] = b
+    if (code == 1 || code == 3 || code == 4 || code == 5) open(1);  // tn[3], tn[4] = a0, a1
+    if (code == 2 || code == 6 || code == 7) open(2);                // tn[3], tn[4] = b0, b1
+    if (code == 3) open(2);
+    if (code == 4 || code == 6) open(3);
+    if (code == 5 || code == 7) open(4);
+    // depth-first frontier of the treelet, each opened node's children swapped when `flip` says so
+    auto frontier = [&](auto &&flip, int out[4]) {
+        int st[8], sp = 0, n = 0;
+        st[sp++] = 0;
+        while (sp) {
+            const int i = st[--sp];
+            if (tn[i].kid[0] < 0) {
+                out[n++] = i;
+                continue;
+            }
+            const bool f = flip(tn[i].axis);
+            st[sp++] = tn[i].kid[f ? 0 : 1];
+            st[sp++] = tn[i].kid[f ? 1 : 0];
+        }
+        return n;
+    };
+    int slot_tn[4];
+    const int n_slots = frontier([](uint32_t) { return false; }, slot_tn);
+    for (int s = 0; s < 4; s++) slot_ref2[s] = AKR_CHILD_EMPTY;
+    for (int s = 0; s < n_slots; s++) {
+        slot_ref2[s] = tn[slot_tn[s]].ref;
+        slot_box[s] = tn[slot_tn[s]].box;
     }
-    return 0;
+    order[0] = order[1] = 0;
+    for (uint32_t o = 0; o < 8; o++) {
+        int seq[4];
+        frontier([o](uint32_t axis) { return !((o >> axis) & 1u); }, seq);
+        uint32_t byte = 0, used = 0;
+        for (int s = 0; s < n_slots; s++)
+            for (int p = 0; p < n_slots; p++)
+                if (seq[p] == slot_tn[s]) {
+                    byte |= (uint32_t)p << (2 * s);
+                    used |= 1u << p;
+                }
+        for (int s = n_slots, p = 0; s < 4; s++) {  // empty slots: the positions left (never entered)
+            while (used & (1u << p)) p++;
+            byte |= (uint32_t)p << (2 * s);
+            used |= 1u << p;
+        }
+        order[o >> 2] |= byte << (8 * (o & 3));
+    }
+    return n_slots;
 }
 
 // Layout: wide nodes in depth-first preorder (a node, then its slots' subtrees in slot order) and
@@ -85,7 +138,68 @@ int gather_slots(const std::vector<akr_bvh_node> &in, uint32_t n2, uint32_t slot
 struct Collapser {
     const std::vector<akr_bvh_node> &in;
     Bvh4Output &out;
+    int collapse;
     std::vector<uint32_t> n_nodes, n_leaves;  // per BVH2 node: wide nodes / leaves of its wide subtree
+    std::vector<uint8_t> choice;              // AKR_COLLAPSE_SAH: per BVH2 node, its treelet code
+
+    bool internal(uint32_t r) const { return r != AKR_CHILD_EMPTY && !(r & AKR_CHILD_LEAF); }
+
+    int code_of(uint32_t n2) const {
+        if (collapse == AKR_COLLAPSE_SAH) return choice[n2];
+        const bool ia = internal(in[n2].child[0]), ib = internal(in[n2].child[1]);  // balanced
+        return ia && ib ? 3 : (ia ? 1 : (ib ? 2 : 0));
+    }
+
+    // AKR_COLLAPSE_SAH: the treelet of every node that minimises the expected number of wide-node
+    // visits of its subtree, sum over wide nodes of the area of their box (a ray's chance to enter
+    // it), by dynamic programming from the leaves up.  Leaves do not enter the sum: every leaf is a
+    // slot of exactly one wide node whatever the treelets, and is tested when that slot is entered.
+    // cost[x] = the sum for the wide subtree below a wide node rooted at x (x's own area excluded).
+    void choose(uint32_t root) {
+        choice.assign(in.size(), 0);
+        std::vector<double> cost(in.size(), 0.0);
+        auto area = [](const Box &b) {
+            const double dx = (double)b.hi[0] - b.lo[0], dy = (double)b.hi[1] - b.lo[1], dz = (double)b.hi[2] - b.lo[2];
+            return dx * dy + dy * dz + dz * dx;
+        };
+        // a frontier entry: child c of node p, reached as a wide node of its own when internal
+        auto G = [&](uint32_t p, int c) {
+            const uint32_t r = in[p].child[c];
+            return internal(r) ? area(child_box(in[p], c)) + cost[r] : 0.0;
+        };
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            auto [n, done] = st.back();
+            st.pop_back();
+            const uint32_t a = in[n].child[0], b = in[n].child[1];
+            if (!done) {
+                st.push_back({n, true});
+                if (internal(a)) st.push_back({a, false});
+                if (internal(b)) st.push_back({b, false});
+                continue;
+            }
+            const bool ia = internal(a), ib = internal(b);
+            double c[8];
+            for (double &x : c) x = INFINITY;
+            c[0] = G(n, 0) + G(n, 1);
+            if (ia) {
+                c[1] = G(a, 0) + G(a, 1) + G(n, 1);
+                if (internal(in[a].child[0])) c[4] = G(in[a].child[0], 0) + G(in[a].child[0], 1) + G(a, 1) + G(n, 1);
+                if (internal(in[a].child[1])) c[5] = G(a, 0) + G(in[a].child[1], 0) + G(in[a].child[1], 1) + G(n, 1);
+            }
+            if (ib) {
+                c[2] = G(n, 0) + G(b, 0) + G(b, 1);
+                if (internal(in[b].child[0])) c[6] = G(n, 0) + G(in[b].child[0], 0) + G(in[b].child[0], 1) + G(b, 1);
+                if (internal(in[b].child[1])) c[7] = G(n, 0) + G(b, 0) + G(in[b].child[1], 0) + G(in[b].child[1], 1);
+            }
+            if (ia && ib) c[3] = G(a, 0) + G(a, 1) + G(b, 0) + G(b, 1);
+            int best = 0;
+            for (int k = 1; k < 8; k++)
+                if (c[k] < c[best]) best = k;
+            choice[n] = (uint8_t)best;
+            cost[n] = c[best];
+        }
+    }
 
     struct Task {
         uint32_t n2, node_at, leaf_at;
@@ -97,12 +211,12 @@ struct Collapser {
         n_nodes.assign(in.size(), 0);
         n_leaves.assign(in.size(), 0);
         std::vector<std::pair<uint32_t, bool>> st{{root, false}};
-        uint32_t ref[4], axis[3];
+        uint32_t ref[4], order[2];
         Box box[4];
         while (!st.empty()) {
             auto [n2, done] = st.back();
             st.pop_back();
-            gather_slots(in, n2, ref, box, axis);
+            gather_slots(in, n2, code_of(n2), ref, box, order);
             if (!done) {
                 st.push_back({n2, true});
                 for (int s = 0; s < 4; s++)
@@ -139,9 +253,9 @@ struct Collapser {
     template <class Spawn>
     void build(const Task &t, int &max_depth, float &max_abs, uint32_t spawn_below, Spawn &&spawn) {
         if (t.depth > max_depth) max_depth = t.depth;
-        uint32_t slot_ref2[4], axis[3];
+        uint32_t slot_ref2[4], order[2];
         Box slot_box[4];
-        gather_slots(in, t.n2, slot_ref2, slot_box, axis);
+        gather_slots(in, t.n2, code_of(t.n2), slot_ref2, slot_box, order);
         // quantization frame: the union of the slot boxes
         float plo[3], phi[3];
         for (int k = 0; k < 3; k++) {
@@ -182,7 +296,9 @@ struct Collapser {
             max_abs = std::max(max_abs, std::max(std::fabs(plo[k]), pow2f(e)));
             ex[k] = (uint32_t)(e + 127);
         }
-        w.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | (axis[0] | axis[1] << 2 | axis[2] << 4) << 24;
+        w.meta = ex[0] | ex[1] << 8 | ex[2] << 16;
+        w.order[0] = order[0];
+        w.order[1] = order[1];
         uint32_t node_at = t.node_at + 1, leaf_at = t.leaf_at;
         for (int s = 0; s < 4; s++) {
             const uint32_t r = slot_ref2[s];
@@ -211,6 +327,7 @@ struct Collapser {
     }
 
     void run(uint32_t root, int threads) {
+        if (collapse == AKR_COLLAPSE_SAH) choose(root);
         count(root);
         out.nodes.resize(n_nodes[root]);
         out.leaves.resize(n_leaves[root]);
@@ -319,7 +436,7 @@ int validate_bvh2(const akr_bvh_node *nodes, uint64_t n_nodes, const akr_bvh_tri
     return depth;
 }
 
-void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads) {
+void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_threads, int collapse) {
     out.nodes.clear();
     out.leaves.clear();
     out.max_depth = 0;
@@ -331,11 +448,11 @@ void build_bvh4(const std::vector<akr_bvh_node> &bvh2, Bvh4Output &out, int n_th
     if (r == AKR_CHILD_EMPTY) return;
     if (r & AKR_CHILD_LEAF) {
         out.leaves.resize(1);
-        Collapser c{bvh2, out, {}, {}};
+        Collapser c{bvh2, out, collapse, {}, {}, {}};
         c.put_leaf(0, r, child_box(vroot, 0));
         out.root_ref = AKR_CHILD_LEAF;
     } else {
-        Collapser c{bvh2, out, {}, {}};
+        Collapser c{bvh2, out, collapse, {}, {}, {}};
         c.run(r, n_threads);
         out.root_ref = 0;
     }

@@ -317,6 +317,7 @@ struct akr_hip_ctx {
     int shadow_grid_pct = 100;  // persistent shadow-trace grid as a percentage of the resident maximum
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
+    int wide_collapse = AKR_COLLAPSE_SAH;  // akr_build_params::wide_collapse of the last build
     bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
     DBuf<uint32_t> d_steps;
     uint64_t n_steps = 0;
@@ -1386,7 +1387,7 @@ namespace {
 // itself for the exact lane path, the accel info, and the scene's shading records.
 void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         auto &b = ctx->bvh;
-        build_bvh4(b.nodes, ctx->bvh4, n_threads);
+        build_bvh4(b.nodes, ctx->bvh4, n_threads, ctx->wide_collapse);
         if (ctx->bvh4.nodes.size() >= kMaxWideNodes)
             throw std::runtime_error("scene too large: the wide view needs fewer than 2^26 nodes (about 100 M triangles)");
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
@@ -1463,6 +1464,9 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         if (p.builder == AKR_BUILDER_LBVH) build_lbvh_gpu(in, ctx->bvh, ctx->stream);
         else if (p.builder == AKR_BUILDER_SAH || p.builder == AKR_BUILDER_SBVH) build_bvh(in, p, ctx->bvh);
         else throw std::runtime_error("unknown builder");
+        if (p.wide_collapse != AKR_COLLAPSE_SAH && p.wide_collapse != AKR_COLLAPSE_BALANCED)
+            throw std::runtime_error("unknown wide_collapse");
+        ctx->wide_collapse = p.wide_collapse;
         finish_accel(ctx, p.n_threads);
     });
 }
@@ -1482,6 +1486,7 @@ int akr_hip_import_accel(akr_hip_ctx *ctx, const void *nodes, uint64_t n_nodes, 
         b.max_leaf = max_leaf;
         b.sah_cost = 0.0;  // not known for an imported tree
         b.build_ms = 0.0;
+        ctx->wide_collapse = AKR_COLLAPSE_SAH;
         finish_accel(ctx, n_threads);
     });
 }
@@ -1747,6 +1752,7 @@ struct akr_bvh_host {
     Bvh4Output wide;
     bool wide_built = false;
     int n_threads = 0;  // the build's thread count, used by the wide collapse too
+    int collapse = AKR_COLLAPSE_SAH;
 };
 
 int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t *indices, uint64_t n_triangles,
@@ -1764,6 +1770,8 @@ int akr_bvh_host_build(const float *vertices, uint64_t n_vertices, const int32_t
         if (params) p = *params;
         std::unique_ptr<akr_bvh_host> h(new akr_bvh_host());
         h->n_threads = p.n_threads;
+        if (p.wide_collapse != AKR_COLLAPSE_SAH && p.wide_collapse != AKR_COLLAPSE_BALANCED) return -1;
+        h->collapse = p.wide_collapse;
         BvhInput in{vertices, indices, n_triangles};
         build_bvh(in, p, h->out);
         if (info) {
@@ -1802,7 +1810,7 @@ int akr_bvh_host_wide(akr_bvh_host *h, uint64_t *n_nodes, uint64_t *n_leaves, ui
     if (!h) return -1;
     try {
         if (!h->wide_built) {
-            build_bvh4(h->out.nodes, h->wide, h->n_threads);
+            build_bvh4(h->out.nodes, h->wide, h->n_threads, h->collapse);
             h->wide_built = true;
         }
         if (n_nodes) *n_nodes = h->wide.nodes.size();

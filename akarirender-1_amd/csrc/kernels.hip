@@ -213,22 +213,18 @@ __device__ __forceinline__ float ubyte(uint32_t w, int k) {  // v_cvt_f32_ubyte{
 
 // Continue with the first entered slot of a wide node in the BVH2 depth-first order and push the
 // other entered slots behind it, each with its entry distance; pop when no slot is entered.
-// `dpos` holds the ray's direction signs: bit a = (d[a] > 0).  The order is a permutation of the
-// slots by three flip bits (near = left iff d[axis] > 0 at each of the three folded BVH2 nodes):
-// position(slot k) = k ^ (f0 << 1 | f_{1 + k/2}).  Entered slots are ranked by position without
-// moving any data: the first becomes `cur`, each other one is written straight to its stack entry
-// sp + (number of entered slots at later positions), so the earliest is popped first.
+// `dpos` holds the ray's direction signs: bit a = (d[a] > 0), the octant.  The node's order words
+// (akr_bvh4_node::order) give each slot's position in the depth-first order of that octant: byte
+// dpos, two bits per slot.  Entered slots are ranked by position without moving any data: the first
+// becomes `cur`, each other one is written straight to its stack entry sp + (number of entered
+// slots at later positions), so the earliest is popped first.
 template <bool ANY>
-__device__ __forceinline__ void wide_order_push(uint32_t meta, uint32_t dpos, const float (&t)[4], const bool (&hit)[4],
-                                                const uint32_t (&ref)[4], uint32_t &cur, float lim, lds_u64 *s_stack,
-                                                glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
-                                                int &sp) {
-    const uint32_t ax = meta >> 24;
-    const uint32_t f0 = ~(dpos >> (ax & 3u)) & 1u;
-    const uint32_t f1 = ~(dpos >> ((ax >> 2) & 3u)) & 1u;
-    const uint32_t f2 = ~(dpos >> ((ax >> 4) & 3u)) & 1u;
-    const uint32_t m01 = (f0 << 1) | f1, m23 = (f0 << 1) | f2;
-    const uint32_t pos[4] = {m01, 1u ^ m01, 2u ^ m23, 3u ^ m23};
+__device__ __forceinline__ void wide_order_push(uint32_t order_lo, uint32_t order_hi, uint32_t dpos, const float (&t)[4],
+                                                const bool (&hit)[4], const uint32_t (&ref)[4], uint32_t &cur, float lim,
+                                                lds_u64 *s_stack, glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid,
+                                                uint32_t gtid, int &sp) {
+    const uint32_t perm = ((dpos & 4u) ? order_hi : order_lo) >> ((dpos & 3u) << 3);
+    const uint32_t pos[4] = {perm & 3u, (perm >> 2) & 3u, (perm >> 4) & 3u, (perm >> 6) & 3u};
     uint32_t pm = 0;  // entered slots, by position
 #pragma unroll
     for (int k = 0; k < 4; k++) pm |= hit[k] ? (1u << pos[k]) : 0u;
@@ -275,7 +271,7 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
     const float4 h = *reinterpret_cast<const float4 *>(wb + off);       // origin.xyz, meta
     const uint4 c = *reinterpret_cast<const uint4 *>(wb + off + 16);    // slot refs
     const uint4 qa = *reinterpret_cast<const uint4 *>(wb + off + 32);   // qlo_x, qhi_x, qlo_y, qhi_y
-    const uint4 qb = *reinterpret_cast<const uint4 *>(wb + off + 48);   // qlo_z, qhi_z
+    const uint4 qb = *reinterpret_cast<const uint4 *>(wb + off + 48);   // qlo_z, qhi_z, order[2]
     const uint32_t meta = __float_as_uint(h.w);
     const float sx = __uint_as_float((meta & 0xFFu) << 23);
     const float sy = __uint_as_float(((meta >> 8) & 0xFFu) << 23);
@@ -295,7 +291,7 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, lim, s_stack, ovf, ovf_threads, tid, gtid, sp);
+    wide_order_push<ANY>(qb.z, qb.w, dpos, t, hit, ref, cur, lim, s_stack, ovf, ovf_threads, tid, gtid, sp);
     return tested;
 }
 
@@ -368,7 +364,8 @@ __device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, 
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    wide_order_push<ANY>(meta, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid, sp);
+    wide_order_push<ANY>(qb.z, qb.w, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid,
+                         sp);
     return tested;
 }
 

@@ -48,20 +48,21 @@ typedef struct akr_bvh_tri {
 } akr_bvh_tri;
 
 /* Wide (4-child) view of the same tree, which the traversal kernels walk.
- * A wide node is one BVH2 node with its two children collapsed into it: slots 0, 1 are the left
- * child's children (or the left child itself, slot 1 EMPTY, when it is a leaf), slots 2, 3 the
- * right child's; axis0/1/2 are the split axes of the three BVH2 nodes, so the BVH2 depth-first
- * order of the four slots follows from the ray direction.  Slot boxes are quantized OUTWARD to
+ * A wide node is a treelet of at most three BVH2 internal nodes (a node and up to two nodes below
+ * it, chosen by surface area) whose frontier children are its slots, stored in the treelet's
+ * depth-first order.  order[] gives, for each ray direction octant o (bit a = d[a] > 0), the slots'
+ * positions in the BVH2 depth-first order for that octant (near = left iff d[axis] > 0 at every
+ * node of the treelet): byte o of the pair, two bits per slot.  Slot boxes are quantized OUTWARD to
  * 8 bits per bound: bound = fmaf(q, 2^(e - 127), origin) is <= (lo) / >= (hi) the exact bound, so
  * a slot test can only pass more often than the exact one.  Every leaf keeps its exact f32 box in
  * an akr_bvh_leaf record and is tested with it (with the current best t) before its triangles:
  * the leaves whose triangles are tested, and their order, are exactly the BVH2 traversal's. */
 typedef struct akr_bvh4_node {
     float origin[3];
-    uint32_t meta;     /* ex | ey << 8 | ez << 16 | (axis0 | axis1 << 2 | axis2 << 4) << 24 */
+    uint32_t meta;     /* ex | ey << 8 | ez << 16 (frame step exponents, biased by 127) */
     uint32_t child[4]; /* wide node index, AKR_CHILD_LEAF | leaf index, or AKR_CHILD_EMPTY */
     uint32_t q[6];     /* qlo_x, qhi_x, qlo_y, qhi_y, qlo_z, qhi_z; byte k of each = slot k */
-    uint32_t _pad[2];
+    uint32_t order[2]; /* per octant slot positions: octants 0-3 in order[0], 4-7 in order[1] */
 } akr_bvh4_node;
 
 typedef struct akr_bvh_leaf {

@@ -139,8 +139,11 @@ typedef struct akr_build_params {
     int32_t builder;        /* AKR_BUILDER_SAH (host binned SAH, default), _LBVH (GPU) or _SBVH (host) */
     float spatial_budget;   /* SBVH: extra references allowed, as a fraction of the triangles
                              * (0 = default 0.5) */
-    int32_t _pad;
+    int32_t wide_collapse;  /* the traversal's 4-wide view: AKR_COLLAPSE_SAH (0,
+                             * default) or AKR_COLLAPSE_BALANCED */
 } akr_build_params;
+#define AKR_COLLAPSE_SAH 0       /* treelets of up to 3 BVH2 nodes chosen for the fewest expected visits */
+#define AKR_COLLAPSE_BALANCED 1  /* a wide node folds in only its own internal children */
 #define AKR_BUILDER_SAH 0
 #define AKR_BUILDER_LBVH 1  /* GPU Morton/Karras build: much faster, lower tree quality */
 #define AKR_BUILDER_SBVH 2  /* host SBVH: the reference's spatial splits (bvh-accelerator.h:125-475) */

@@ -106,27 +106,30 @@ def _wide_walk(wide, signs):
             out.append((ref & 0x7FFFFFFF, path))
             return
         nd = wn[ref]
-        ax = int(nd["meta"]) >> 24
-        f0, f1, f2 = signs[ax & 3], signs[(ax >> 2) & 3], signs[(ax >> 4) & 3]
-        pa = [0, 1] if f1 else [1, 0]
-        pb = [2, 3] if f2 else [3, 2]
+        octant = sum(1 << a for a in range(3) if signs[a])
+        perm = (int(nd["order"][octant >> 2]) >> (8 * (octant & 3))) & 0xFF
+        pos = [(perm >> (2 * k)) & 3 for k in range(4)]
+        assert sorted(pos) == [0, 1, 2, 3]
         boxes = slot_boxes(nd)
-        for k in (pa + pb if f0 else pb + pa):
+        for k in sorted(range(4), key=lambda k: pos[k]):
             visit(int(nd["child"][k]), path + [boxes[k]])
 
     visit(root, [])
     return out
 
 
+@pytest.mark.parametrize("collapse", [capi.COLLAPSE_SAH, capi.COLLAPSE_BALANCED])
 @pytest.mark.parametrize("builder", ["sah", "sbvh"])
 @pytest.mark.parametrize("leaf", [1, 4])
-def test_wide_view_invariants(leaf, builder):
-    """The 4-wide traversal view: every leaf's exact box lies inside every quantized slot box on
-    its path (the wide test can only pass more often), leaf records cover the triangles once, and
-    for every direction octant the leaves come in the BVH2 depth-first order."""
+def test_wide_view_invariants(leaf, builder, collapse):
+    """The 4-wide traversal view (both treelet choices): every leaf's exact box lies inside every
+    quantized slot box on its path (the wide test can only pass more often), leaf records cover the
+    triangles once, every node's order bytes are permutations, and for every direction octant the
+    leaves come in the BVH2 depth-first order."""
     cs = scene.compile_scene(small_soup(5_000, r=0.01 if builder == "sah" else 0.2))
     nodes, tris, info, wide = capi.build_bvh_host(cs.vertices, cs.indices, max_leaf_size=leaf, wide=True,
-                                                  builder=capi.BUILDER_SBVH if builder == "sbvh" else 0)
+                                                  builder=capi.BUILDER_SBVH if builder == "sbvh" else 0,
+                                                  wide_collapse=collapse)
     wn, lv, root = wide
     assert sorted((int(l["first"]), int(l["count"])) for l in lv) == sorted(_bvh2_leaf_order(nodes, (1, 1, 1)))
     for octant in range(8):
