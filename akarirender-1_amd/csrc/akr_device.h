@@ -159,6 +159,8 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     uint32_t any_far_first;        // 1: shadow (boolean occlusion) rays visit the far slots first (order-free)
     TraceCounters *counters;       // [3]: closest, any, shadow
     uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
+    uint32_t step_cap;             // COUNT builds with ray_steps: a ray stops after this many steps (0: none;
+                                   // the cost-ordered fetch's pilot, whose hits nobody reads)
 };
 
 struct ShadeArgs {

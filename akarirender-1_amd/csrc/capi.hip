@@ -213,7 +213,14 @@ struct akr_hip_ctx {
 
     // path / queue buffers
     size_t cap = 0;
+    // The last render's tile list, clipped, non-empty tiles only: (x0, y0, width, first slot).  The
+    // pixel list is expanded from it on the device (k_expand_pixels); the host copy h_pixel is built
+    // only for the host-side merges that need it (host_pixels()).
+    std::vector<uint4> h_tiles;
+    uint64_t n_pix_last = 0;
+    DBuf<uint4> d_tiles;
     std::vector<uint32_t> h_pixel;
+    bool h_pixel_ok = false;
     DBuf<uint32_t> d_pixel, d_seed, d_slot0, d_slot1, d_counts;
     DBuf<float4> d_ray0, d_ray1, d_state0, d_state1, d_hit, d_film;
     DBuf<float4> d_L[2];  // per-sample radiance, alternating by sample pass (passes overlap)
@@ -281,6 +288,10 @@ struct akr_hip_ctx {
     int64_t path_order_share_pixels = 1200000;
     int path_order_share_min_spp = 16;
     int path_order_shift = 2;
+    // option "path_order_cap": a pilot ray stops after this many steps (0: none); its cost class is
+    // then the cap's.  The pilot is a small latency-bound launch whose length is set by its slowest
+    // ray, while the order only needs coarse classes (soup against background).
+    int path_order_cap = 64;
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
     DBuf<TraceCounters> d_ocnt;
@@ -716,28 +727,34 @@ struct akr_hip_ctx {
         t.hits = d_hit.p;
         t.counters = d_ocnt.p;
         t.ray_steps = d_okey[1].p;
+        t.step_cap = (uint32_t)path_order_cap;
         launch_trace(TRACE_CLOSEST, true, true, true, t, grid_for(TRACE_CLOSEST, N), ms);
         launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, d_okey[0].p, d_oidx[0].p, ms);
         sort_pixel_order(d_otmp.p, tb, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
         HIPCHK(hipGetLastError());
     }
 
-    // Pixels of the tile list (tiles in order, row-major inside a tile) into h_pixel / d_pixel;
-    // sizes the queues and the per-pass counter sets.  Returns the pixel count.
-    // look_ok: the render may use lookahead lanes (cur_look); the path buffers are sized for it.
+    // Pixels of the tile list (tiles in order, row-major inside a tile) into d_pixel, expanded on
+    // the device from the clipped tiles (the host loop over every pixel and the pageable upload of
+    // its list cost 1.7 ms per 1080p render); sizes the queues and the per-pass counter sets.
+    // Returns the pixel count.  look_ok: the render may use lookahead lanes (cur_look); the path
+    // buffers are sized for it.
     uint64_t setup_pixels(const akr_rect *tiles, int32_t n_tiles, size_t n_count_words, hipStream_t st,
                           bool look_ok = false) {
         require_ready();
         if (!cam_set) throw std::runtime_error("camera not set (call akr_hip_set_camera)");
         if (n_tiles < 0 || (n_tiles > 0 && !tiles)) throw std::runtime_error("invalid tile list");
-        h_pixel.clear();
+        h_tiles.clear();
+        h_pixel_ok = false;
+        uint64_t N = 0;
         for (int k = 0; k < n_tiles; k++) {
-            int x0 = std::max(0, tiles[k].x0), y0 = std::max(0, tiles[k].y0);
-            int x1 = std::min(cam.width, tiles[k].x1), y1 = std::min(cam.height, tiles[k].y1);
-            for (int y = y0; y < y1; y++)
-                for (int x = x0; x < x1; x++) h_pixel.push_back((uint32_t)x | ((uint32_t)y << 16));
+            const int x0 = std::max(0, tiles[k].x0), y0 = std::max(0, tiles[k].y0);
+            const int x1 = std::min(cam.width, tiles[k].x1), y1 = std::min(cam.height, tiles[k].y1);
+            if (x1 <= x0 || y1 <= y0) continue;
+            if (N >= (1ull << 31)) break;  // rejected below
+            h_tiles.push_back(make_uint4((uint32_t)x0, (uint32_t)y0, (uint32_t)(x1 - x0), (uint32_t)N));
+            N += (uint64_t)(x1 - x0) * (uint64_t)(y1 - y0);
         }
-        const uint64_t N = h_pixel.size();
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
         // lookahead: R active pixels get look_lanes(R) lanes, R * lanes <= max(N, budget + N / 2)
         cur_look = look_ok && lookahead != 1 && look_lanes((uint32_t)N, look_budget(), look_cap()) >= 2;
@@ -746,14 +763,33 @@ struct akr_hip_ctx {
         serialize(st);
         ensure_capacity(cur_slots);  // before any upload: a reallocation drops contents
         d_counts.reserve(2 * n_count_words);
+        n_pix_last = N;
         if (N == 0) return 0;
         ensure_side_stream();
-        HIPCHK(hipMemcpyAsync(d_pixel.p, h_pixel.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        d_tiles.upload(h_tiles.data(), h_tiles.size(), st);
+        launch_expand_pixels(d_tiles.p, (uint32_t)h_tiles.size(), (uint32_t)N, d_pixel.p, st);
+        HIPCHK(hipGetLastError());
         HIPCHK(hipMemsetAsync(d_film.p, 0, N * sizeof(float4), st));
         HIPCHK(hipEventRecord(ev_fork, st));  // both internal streams start after the caller's work
         HIPCHK(hipStreamWaitEvent(main_st, ev_fork, 0));
         HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
         return N;
+    }
+
+    // The last render's pixel list on the host (slot order), for the host-side film merges
+    const std::vector<uint32_t> &host_pixels() {
+        if (!h_pixel_ok) {
+            h_pixel.resize(n_pix_last);
+            for (const uint4 &t : h_tiles) {
+                const uint64_t end = &t == &h_tiles.back() ? n_pix_last : (&t)[1].w;
+                for (uint64_t i = t.w; i < end; i++) {
+                    const uint32_t local = (uint32_t)(i - t.w);
+                    h_pixel[i] = (t.x + local % t.z) | ((t.y + local / t.z) << 16);
+                }
+            }
+            h_pixel_ok = true;
+        }
+        return h_pixel;
     }
 
     // order `st` after the context's previous trace / render ("one context, one
@@ -1271,6 +1307,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_share_min_spp") {
             if (value < 0) throw std::runtime_error("path_order_share_min_spp must be >= 0");
             ctx->path_order_share_min_spp = (int)std::min<int64_t>(value, INT32_MAX);
+        } else if (k == "path_order_cap") {
+            if (value < 0 || value > INT32_MAX) throw std::runtime_error("path_order_cap must be in [0, 2^31)");
+            ctx->path_order_cap = (int)value;
         } else if (k == "path_order_shift") {
             if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
             ctx->path_order_shift = (int)value;
@@ -1609,8 +1648,9 @@ int akr_hip_render_node(akr_hip_ctx *const *ctxs, int32_t n_ctx, const akr_pt_pa
             if (N == 0) continue;
             std::fill(seen.begin(), seen.end(), 0u);
             std::vector<std::vector<uint32_t>> rank;
+            const std::vector<uint32_t> &pl = ctxs[k]->host_pixels();
             for (uint64_t i = 0; i < N; i++) {
-                const uint32_t px = ctxs[k]->h_pixel[i];
+                const uint32_t px = pl[i];
                 const uint64_t p = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
                 const uint32_t r = seen[p]++;
                 if (r >= rank.size()) rank.emplace_back();
@@ -1706,8 +1746,9 @@ void merge_film(akr_hip_ctx *ctx, uint64_t N, int spp, float *radiance, float *w
                                           " pixels do not hold " + std::to_string(spp) + " samples");
     }
     const int W = ctx->cam.width;
+    const std::vector<uint32_t> &pl = ctx->host_pixels();
     for (uint64_t k = 0; k < N; k++) {
-        uint32_t px = ctx->h_pixel[k];
+        uint32_t px = pl[k];
         uint64_t pix = (uint64_t)(px & 0xFFFFu) + (uint64_t)(px >> 16) * W;
         radiance[3 * pix + 0] += film[k].x;
         radiance[3 * pix + 1] += film[k].y;

@@ -25,6 +25,7 @@ void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t
 void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t *order, uint32_t n, int32_t width,
                        float *rad, float *w, hipStream_t st);
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st);
+void launch_expand_pixels(const uint4 *tiles, uint32_t n_tiles, uint32_t n, uint32_t *pixel, hipStream_t st);
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st);
 // cost-ordered pixel fetch: pilot camera rays, sort keys, and the stable key sort (lbvh.hip, rocPRIM)
 constexpr uint32_t kOrderClassBits = 12, kOrderClassMask = (1u << kOrderClassBits) - 1u;

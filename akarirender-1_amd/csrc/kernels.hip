@@ -600,6 +600,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                         c_box += nt;
                         c_visit++;
                         deep = deep || sp > kStackLds;
+                        if (a.step_cap && steps >= a.step_cap) cur = AKR_CHILD_EMPTY;  // pilot: cost capped
                     }
                 } else if (!WIDE && busy && is_internal(cur)) {
                     if (COUNT) {
@@ -2240,6 +2241,24 @@ __global__ __launch_bounds__(kBlock) void k_merge_film(const float4 *film, const
     w[p] += f.w;
 }
 
+// The render's pixel list from its tile list, on the device: `tiles` holds each non-empty clipped
+// tile as (x0, y0, width, first slot), in list order; slot i lies in the last tile whose first slot
+// is <= i, row-major inside it (the order the host list had, capi.hip setup_pixels).  One thread
+// per slot, a binary search over the (few thousand) tiles, which stay in L2.
+__global__ __launch_bounds__(kBlock) void k_expand_pixels(const uint4 *tiles, uint32_t n_tiles, uint32_t n,
+                                                          uint32_t *pixel) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint32_t lo = 0, hi = n_tiles;  // largest k with tiles[k].w <= i (tiles[0].w == 0)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (tiles[mid].w <= i) lo = mid; else hi = mid;
+    }
+    const uint4 t = tiles[lo];
+    const uint32_t local = i - t.w;
+    pixel[i] = (t.x + local % t.z) | ((t.y + local / t.z) << 16);
+}
+
 __global__ __launch_bounds__(kBlock) void k_unpack_film(const float4 *film, uint32_t n, float *rad, float *w) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -2433,6 +2452,9 @@ void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_probe_seed, dim3(blocks_for(n)), dim3(kBlock), 0, st, seed, n, probe);
+}
+void launch_expand_pixels(const uint4 *tiles, uint32_t n_tiles, uint32_t n, uint32_t *pixel, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_expand_pixels, dim3(blocks_for(n)), dim3(kBlock), 0, st, tiles, n_tiles, n, pixel);
 }
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st) {
     if (n == 0) return;
