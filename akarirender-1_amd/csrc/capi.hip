@@ -292,6 +292,9 @@ struct akr_hip_ctx {
     // then the cap's.  The pilot is a small latency-bound launch whose length is set by its slowest
     // ray, while the order only needs coarse classes (soup against background).
     int path_order_cap = 64;
+    // option "path_order_sub": one pilot ray per 2^path_order_sub slots (neighbours in a tile row
+    // share its cost); 0 = a pilot ray per slot
+    int path_order_sub = 0;
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
     DBuf<TraceCounters> d_ocnt;
@@ -720,16 +723,17 @@ struct akr_hip_ctx {
         if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
         const size_t tb = d_otmp.n;
         HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
-        launch_pilot_rays(cam, d_pixel.p, N, d_ray0.p, ms);
+        const uint32_t sub = (uint32_t)path_order_sub, n_rays = (uint32_t)(((uint64_t)N + (1u << sub) - 1) >> sub);
+        launch_pilot_rays(cam, d_pixel.p, n_rays, sub, d_ray0.p, ms);
         TraceArgs t = trace_args(d_owork.p);
         t.rays = d_ray0.p;
-        t.n = N;
+        t.n = n_rays;
         t.hits = d_hit.p;
         t.counters = d_ocnt.p;
         t.ray_steps = d_okey[1].p;
         t.step_cap = (uint32_t)path_order_cap;
-        launch_trace(TRACE_CLOSEST, true, true, true, t, grid_for(TRACE_CLOSEST, N), ms);
-        launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, d_okey[0].p, d_oidx[0].p, ms);
+        launch_trace(TRACE_CLOSEST, true, true, true, t, grid_for(TRACE_CLOSEST, n_rays), ms);
+        launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, sub, d_okey[0].p, d_oidx[0].p, ms);
         sort_pixel_order(d_otmp.p, tb, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
         HIPCHK(hipGetLastError());
     }
@@ -1310,6 +1314,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_cap") {
             if (value < 0 || value > INT32_MAX) throw std::runtime_error("path_order_cap must be in [0, 2^31)");
             ctx->path_order_cap = (int)value;
+        } else if (k == "path_order_sub") {
+            if (value < 0 || value > 5) throw std::runtime_error("path_order_sub must be in [0, 5]");
+            ctx->path_order_sub = (int)value;
         } else if (k == "path_order_shift") {
             if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
             ctx->path_order_shift = (int)value;

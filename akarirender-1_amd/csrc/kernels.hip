@@ -2280,10 +2280,13 @@ __global__ __launch_bounds__(kBlock) void k_check_weights(const float4 *film, ui
 // Cost-ordered pixel fetch of the persistent path kernels.  Pilot: the camera ray
 // of each slot's first sample, made from a copy of its seed (nothing is committed), traced by the
 // counting kernel, whose per-ray steps (traversal iterations + triangle tests) rank the pixels.
-__global__ __launch_bounds__(kBlock) void k_pilot_rays(CameraDev cam, const uint32_t *pixel, uint32_t n, float4 *rays) {
+// With `sub` > 0 only every 2^sub-th slot gets a pilot ray (ray k: slot k << sub; neighbours in a
+// tile row share a cost estimate), which shortens the pilot launch.
+__global__ __launch_bounds__(kBlock) void k_pilot_rays(CameraDev cam, const uint32_t *pixel, uint32_t n, uint32_t sub,
+                                                      float4 *rays) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const uint32_t px = pixel[i];
+    const uint32_t px = pixel[i << sub];
     const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
     uint32_t seed = (uint32_t)(x + y * cam.width);
     float4 r0, r1;
@@ -2294,13 +2297,13 @@ __global__ __launch_bounds__(kBlock) void k_pilot_rays(CameraDev cam, const uint
 
 // Sort key of slot i: its XCD shard above its cost class (steps >> shift, capped, descending), so a
 // stable sort orders each shard by decreasing cost and keeps tile order within a class.
-__global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t *key,
-                                                       uint32_t *idx) {
+__global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t sub,
+                                                       uint32_t *key, uint32_t *idx) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     uint32_t sh = 0;
     for (uint32_t k = 1; k < kWorkShards; k++) sh += i >= shard_begin(n, k) ? 1u : 0u;
-    const uint32_t s = steps[i];  // 0xFFFFFFFF: traced by the exact BVH2 walk (rare): costliest class
+    const uint32_t s = steps[i >> sub];  // 0xFFFFFFFF: traced by the exact BVH2 walk (rare): costliest class
     const uint32_t cls = s == 0xFFFFFFFFu ? kOrderClassMask : min(s >> shift, kOrderClassMask);
     key[i] = (sh << kOrderClassBits) | (kOrderClassMask - cls);
     idx[i] = i;
@@ -2441,13 +2444,15 @@ void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t
     if (n == 0) return;
     hipLaunchKernelGGL(k_merge_film, dim3(blocks_for(n)), dim3(kBlock), 0, st, film, pixel, order, n, width, rad, w);
 }
-void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, float4 *rays, hipStream_t st) {
+void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, uint32_t sub, float4 *rays,
+                       hipStream_t st) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_pilot_rays, dim3(blocks_for(n)), dim3(kBlock), 0, st, cam, pixel, n, rays);
+    hipLaunchKernelGGL(k_pilot_rays, dim3(blocks_for(n)), dim3(kBlock), 0, st, cam, pixel, n, sub, rays);
 }
-void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t *key, uint32_t *idx, hipStream_t st) {
+void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t sub, uint32_t *key, uint32_t *idx,
+                       hipStream_t st) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift, key, idx);
+    hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift, sub, key, idx);
 }
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st) {
     if (n == 0) return;

@@ -348,6 +348,7 @@ def main():
     npix = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles)
     maxpix = max(sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in tiles_for_rank(W, H, args.tile, r, split))
                  for r in range(split))
+    tiles = capi.rect_array(tiles)   # the C-ABI's akr_rect array, made once (not inside the timed region)
     film = torch.zeros(maxpix * 4, device=dev)          # [radiance rgb (packed) | weight]
     rad, wgt = film[:maxpix * 3], film[maxpix * 3:]
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -23,6 +23,22 @@ def test_library_exports_every_declared_symbol():
     assert capi.load_library().akr_hip_api_version() == 2
 
 
+def test_tile_arrays_pass_without_copy():
+    """render calls take the tile list as an (n, 4) int32 array from capi.rect_array without a
+    copy (the bench converts once, outside its timed region), or as a list of tuples."""
+    tiles = [(0, 0, 32, 32), (32, 0, 40, 17), (-5, 3, 7, 9)]
+    arr = capi.rect_array(tiles)
+    assert arr.dtype == np.int32 and arr.shape == (3, 4) and arr.flags.c_contiguous
+    got, n = capi.HipContext._rects(arr)
+    assert got is arr and n == 3
+    lst, n2 = capi.HipContext._rects(tiles)
+    assert n2 == 3 and [(r.x0, r.y0, r.x1, r.y1) for r in lst] == tiles
+    assert capi._arr_ptr(arr).value == arr.ctypes.data
+    for bad in (arr.astype(np.int64), arr[:, :3].copy(), np.asfortranarray(np.tile(arr, (1, 2))[:, ::2])):
+        with pytest.raises(ValueError):
+            capi.HipContext._rects(bad)
+
+
 def test_create_without_device_fails_cleanly():
     if capi.device_count() > 0:
         pytest.skip("a device is visible")

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--opts", default="", help="library options 'key=v;key2=v'")
     ap.add_argument("--profile-spp", type=int, default=20, help="counted phase profile at this spp (0: none)")
+    ap.add_argument("--sweep", default="", help="one library option swept in-process: 'key=v1,v2,...'")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -41,12 +42,17 @@ def main():
     film = torch.zeros(4 * W * H, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     spps = [int(x) for x in args.spps.split(",")]
-    for n_split in (int(x) for x in args.splits.split(",")):
+    sweep = [(args.sweep.split("=")[0], int(v)) for v in args.sweep.split("=")[1].split(",")] if args.sweep else [None]
+    for n_split, sw in ((n, sw) for n in (int(x) for x in args.splits.split(",")) for sw in sweep):
+        if sw:
+            ctx.set_option(*sw)
+            print(f"-- {sw[0]} = {sw[1]}", flush=True)
         tiles = dist.tile_grid(W, H, 32) if n_split == 1 else dist.tiles_for_rank(W, H, 32, 0, n_split)
         n = dist.n_pixels(tiles)
+        rt = capi.rect_array(tiles)  # as the bench passes it
 
         def render(spp):
-            ctx.render_device(spp, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
+            ctx.render_device(spp, 5, rt, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
 
         render(2)
         torch.cuda.synchronize(dev)
