@@ -1451,7 +1451,11 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
             words += 2 + 3 * (size_t)leaves[i].count;
         }
         if (words >= AKR_CHILD_LEAF) throw std::runtime_error("BVH too large for the wide leaf blob");
-        std::unique_ptr<float4[]> blob(new float4[std::max<size_t>(words, 1)]);
+        // zero float4 of padding behind the last leaf: a leaf phase fetches the second triangle
+        // record with the header whatever the leaf's count (kernels.hip path_leaf)
+        const size_t pad = 3;
+        std::unique_ptr<float4[]> blob(new float4[words + pad]);
+        std::memset(static_cast<void *>(blob.get() + words), 0, sizeof(float4) * pad);
         const float4 *tri4 = reinterpret_cast<const float4 *>(b.tris.data());
         std::vector<akr_bvh4_node> wn = ctx->bvh4.nodes;
         auto remap = [&](uint32_t r) {
@@ -1483,7 +1487,7 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
         ctx->d_wleaves.reserve(1);
         ctx->d_wnodes.upload(wn.data(), wn.size(), ctx->stream);
-        ctx->d_wleaves.upload(blob.get(), words, ctx->stream);
+        ctx->d_wleaves.upload(blob.get(), words + pad, ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));  // before the host staging vectors go away
         ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));
