@@ -167,32 +167,72 @@ def spawn_ranks(n: int, argv, need_devices: bool = True) -> int:
     return subprocess.run(cmd).returncode
 
 
-def build_once_per_node(rank: int, build, export, adopt, barrier, tag: str, shm_dir: Path = Path("/dev/shm")):
-    """Rank 0 runs `build()` and leaves the BVH2 that `export()` returns in shared memory (one .npy
-    per array, written under a temporary name and renamed); after a barrier the other ranks map the
-    files and run `adopt(nodes, tris)`; after a second barrier rank 0 removes them.  Returns what
-    build / adopt returned."""
-    base = shm_dir / f"akr_bench_bvh_{tag}"
-    path = lambda name: Path(f"{base}_{name}.npy")
-    info = None
+def _bcast_from_rank0(obj):
+    """Rank 0's `obj` on every rank (torch.distributed, the live group's backend)."""
+    import torch.distributed as dist
+    box = [obj]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def build_once_per_node(rank: int, build, export, adopt, barrier, tag: str, shm_dir: Path = Path("/dev/shm"),
+                        fallback_dirs=None, bcast=None):
+    """Rank 0 runs `build()` and leaves the BVH2 that `export()` returns in files (one .npy per array,
+    written under a temporary name and renamed): in `shm_dir` when it has room, else in the first
+    `fallback_dirs` entry that has (default: the temp dir; a container's /dev/shm may be 64 MB while
+    the C3 BVH2 is 1.5 GB).  Rank 0 then broadcasts where the files are (`bcast`, default
+    torch.distributed.broadcast_object_list), so a failed or impossible share never leaves a rank
+    waiting: the other ranks map the files and run `adopt(nodes, tris)`, or run `build()` themselves
+    when no directory had room, or raise when rank 0's build failed.  After a barrier rank 0 removes
+    the files.  Returns what build / adopt returned."""
+    bcast = bcast or _bcast_from_rank0
+    dirs = [Path(shm_dir)] + [Path(d) for d in (fallback_dirs if fallback_dirs is not None
+                                                 else [__import__("tempfile").gettempdir()])]
+    names = ("nodes", "tris")
+    files = lambda base: [Path(f"{base}_{n}{suf}.npy") for n in names for suf in ("", ".tmp")]
+    info, where, err = None, None, None
     if rank == 0:
-        info = build()
-        nodes, tris = export()
-        for name, a in (("nodes", nodes), ("tris", tris)):
-            tmp = Path(f"{base}_{name}.tmp.npy")
-            np.save(tmp, a)
-            os.replace(tmp, path(name))
-        del nodes, tris
+        try:
+            info = build()
+            nodes, tris = export()
+            need = nodes.nbytes + tris.nbytes + (64 << 20)
+            for d in dirs:
+                base = d / f"akr_bench_bvh_{tag}"
+                try:
+                    if __import__("shutil").disk_usage(d).free < need:
+                        log(f"[rank 0] BVH share: {d} has less than {need >> 20} MB free")
+                        continue
+                    for name, a in zip(names, (nodes, tris)):
+                        tmp = Path(f"{base}_{name}.tmp.npy")
+                        np.save(tmp, a)
+                        os.replace(tmp, Path(f"{base}_{name}.npy"))
+                    where = str(base)
+                    break
+                except OSError as e:
+                    log(f"[rank 0] BVH share: {d} failed ({e})")
+                    for f in files(base):
+                        f.unlink(missing_ok=True)
+            del nodes, tris
+        except Exception as e:  # tell the other ranks before failing, so none waits for the files
+            err = f"{type(e).__name__}: {e}"
+            bcast({"where": None, "error": err})
+            raise
+    msg = bcast({"where": where, "error": err} if rank == 0 else None)
+    if msg["error"]:
+        raise RuntimeError(f"rank 0 failed to build the BVH: {msg['error']}")
     try:
-        barrier()
         if rank != 0:
-            info = adopt(np.load(path("nodes"), mmap_mode="r"), np.load(path("tris"), mmap_mode="r"))
+            if msg["where"]:
+                base = msg["where"]
+                info = adopt(np.load(f"{base}_nodes.npy", mmap_mode="r"), np.load(f"{base}_tris.npy", mmap_mode="r"))
+            else:
+                log(f"[rank {rank}] BVH share: no room to share, building locally")
+                info = build()
         barrier()
     finally:  # the files hold ~1.5 GB of host memory: rank 0 removes them however the others fared
-        if rank == 0:
-            for name in ("nodes", "tris"):
-                path(name).unlink(missing_ok=True)
-                Path(f"{base}_{name}.tmp.npy").unlink(missing_ok=True)
+        if rank == 0 and where:
+            for f in files(where):
+                f.unlink(missing_ok=True)
     return info
 
 

@@ -98,7 +98,7 @@ print("LAUNCHER-CLEAN")
     assert r.returncode == 0 and "LAUNCHER-CLEAN" in r.stdout, r.stderr[-3000:]
 
 
-def _share_worker(rank, world, port, shm_dir, out_dir):
+def _share_worker(rank, world, port, shm_dir, out_dir, fallback=None):
     import os as _os
     import torch.distributed as dist
     import numpy as _np
@@ -115,7 +115,8 @@ def _share_worker(rank, world, port, shm_dir, out_dir):
     info = b.build_once_per_node(rank, build=lambda: calls.append("build") or "built", export=lambda: (nodes, tris),
                                  adopt=lambda n, t: calls.append("adopt") or (n.tobytes() == nodes.tobytes() and
                                                                               t.tobytes() == tris.tobytes()),
-                                 barrier=dist.barrier, tag="t", shm_dir=Path(shm_dir))
+                                 barrier=dist.barrier, tag="t", shm_dir=Path(shm_dir),
+                                 fallback_dirs=None if fallback is None else [Path(d) for d in fallback])
     dist.barrier()
     Path(out_dir, f"r{rank}").write_text(f"{info}|{','.join(calls)}")
     dist.destroy_process_group()
@@ -132,3 +133,23 @@ def test_bvh_built_once_per_node(tmp_path):
     assert (out / "r0").read_text() == "built|build"
     assert (out / "r1").read_text() == (out / "r2").read_text() == "True|adopt"
     assert list(shm.iterdir()) == []
+
+
+def test_bvh_share_falls_back_when_shm_has_no_room(tmp_path):
+    """A /dev/shm that cannot hold the files (here: missing) sends them to the next directory; when no
+    directory can, the other ranks build the BVH themselves instead of waiting (gloo, 2 ranks)."""
+    import torch.multiprocessing as mp
+    alt, out = tmp_path / "alt", tmp_path / "out"
+    alt.mkdir()
+    out.mkdir()
+    mp.spawn(_share_worker, args=(2, bench._free_port(), str(tmp_path / "missing"), str(out), [str(alt)]),
+             nprocs=2, join=True)
+    assert (out / "r0").read_text() == "built|build"
+    assert (out / "r1").read_text() == "True|adopt"
+    assert list(alt.iterdir()) == []
+    out2 = tmp_path / "out2"
+    out2.mkdir()
+    mp.spawn(_share_worker, args=(2, bench._free_port(), str(tmp_path / "missing"), str(out2),
+                                  [str(tmp_path / "missing2")]), nprocs=2, join=True)
+    assert (out2 / "r0").read_text() == "built|build"
+    assert (out2 / "r1").read_text() == "built|build"
