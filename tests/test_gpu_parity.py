@@ -86,10 +86,19 @@ def test_trace_builder_independent(hip_ctx_factory):
 
 @pytest.mark.parametrize("leaf", [1, 2, 8])
 def test_trace_leaf_sizes(hip_ctx_factory, leaf):
+    """Leaves of 1, 2 and up to 8 triangles: the leaf phases fetch the second triangle record with the
+    header whatever the count (a one-triangle leaf reads into the next leaf or the blob's padding), and
+    read the third and later ones in the loop; closest-hit and any-hit traces, and renders through both
+    persistent kernels (final sampler states too)."""
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, small_soup(30_000), max_leaf_size=leaf)
         assert ctx.accel_info().max_leaf <= leaf
         _check_trace(ctx, orc, cs, random_rays(1 << 14, 4, -1.1, 1.1), False)
+        _check_trace(ctx, orc, cs, random_rays(1 << 14, 5, -1.1, 1.1), True)
+        ctx.set_option("path", 1)
+        for defer in (0, 1):
+            ctx.set_option("path_defer", defer)
+            _check_render(ctx, orc, 2, 5, [(0, 0, 96, 54), (40, 20, 75, 50)], 96, 54, probe=True)
 
 
 @pytest.mark.parametrize("n_tris", [1, 2, 37, 100_000])
