@@ -48,18 +48,26 @@ def main():
 
     full = dist.tile_grid(W, H, args.tile)
     step_ms(full, args.warmup)
-    whole = min(step_ms(full, args.steps) for _ in range(args.repeat))
-    print(json.dumps({"split": 1, "ms_per_step": round(whole, 3), "form": ctx.render_form()}), flush=True)
+    runs = [step_ms(full, args.steps) for _ in range(args.repeat)]
+    whole, whole_avg = min(runs), sum(runs) / len(runs)
+    print(json.dumps({"split": 1, "ms_per_step": round(whole, 3), "ms_per_step_avg": round(whole_avg, 3),
+                      "form": ctx.render_form()}), flush=True)
     for n in (int(x) for x in args.splits.split(",")):
-        per = []
+        per, per_avg = [], []
         for r in range(n):
             tiles = dist.tiles_for_rank(W, H, args.tile, r, n)
             step_ms(tiles, args.warmup)
-            per.append(min(step_ms(tiles, args.steps) for _ in range(args.repeat)))
-        worst = max(per)
+            runs = [step_ms(tiles, args.steps) for _ in range(args.repeat)]
+            per.append(min(runs))
+            per_avg.append(sum(runs) / len(runs))
+        worst, worst_avg = max(per), max(per_avg)
+        # best-of-repeats per rank, and the average over repeats (what one N-rank run sees on average)
         print(json.dumps({"split": n, "rank_ms": [round(x, 3) for x in per], "max_ms": round(worst, 3),
                           "mean_ms": round(sum(per) / n, 3), "imbalance": round(worst * n / sum(per), 3),
-                          "projected_speedup": round(whole / worst, 2), "form": ctx.render_form()}), flush=True)
+                          "projected_speedup": round(whole / worst, 2),
+                          "rank_ms_avg": [round(x, 3) for x in per_avg], "max_ms_avg": round(worst_avg, 3),
+                          "projected_speedup_avg": round(whole_avg / worst_avg, 2), "form": ctx.render_form()}),
+              flush=True)
     ctx.close()
 
 
