@@ -274,13 +274,16 @@ struct akr_hip_ctx {
     int path_order = 2;
     // option "path_order_pair": the cost-ordered fetch of k_path_defer pairs each shard's costliest
     // pixels with its cheapest inside a wave (lanes done early take the long pixels' shadow rays)
-    // instead of costliest-first: 1 = on, 0 = off, 2 (default) = on for renders of at most 400 K
+    // instead of costliest-first: 1 = on, 0 = off, 3 = on for k_path too, 2 (default) = on for renders of at most 400 K
     // pixels (measured on C3 at 32 spp, DESIGN.md §3.10: 8-way share 1.007 -> 0.946 ms, 4-way share
     // 1.499 -> 1.548 ms); option "path_prio": waves whose pixels lie in the first path_prio / 256 of
     // a cost-ordered shard run at raised issue priority (0 = off; measured without effect)
     int path_order_pair = 2;
     int path_prio = 0;
-    int path_order_min_spp = 64;
+    // (16: at the driver's 20 spp the order makes the whole 1080p C3 frame 1.6 % faster, pilot included:
+    // 4.905 -> 4.826 ms per spp, three alternating runs each, profiles/r18_order_min_spp_ab.log; it was 64
+    // until the leaf phase fetched two triangles with the header)
+    int path_order_min_spp = 16;
     // renders of at most path_order_share_pixels pixels (a rank's share of a 2-, 4- or 8-way split)
     // take the order from path_order_share_min_spp samples: the pilot's cost shrinks with the pixel
     // count and the launch tail it shortens does not (C3 at 20 spp, DESIGN.md §3.10: 2- / 4- / 8-way
@@ -995,7 +998,8 @@ struct akr_hip_ctx {
                 if (path_order != 0 && (!defer || path_order == 2) && p.spp >= order_min_spp && N >= 2) {
                     timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
                     pa.order = d_oidx[1].p;
-                    const bool pair = defer && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000));
+                    const bool pair = path_order_pair == 3 ||
+                                      (defer && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000)));
                     pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
                     pa.prio = (uint32_t)path_prio;
                 }
@@ -1321,7 +1325,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
             ctx->path_order_shift = (int)value;
         } else if (k == "path_order_pair") {
-            if (value < 0 || value > 2) throw std::runtime_error("path_order_pair must be 0, 1 or 2 (auto)");
+            if (value < 0 || value > 3)
+                throw std::runtime_error("path_order_pair must be 0, 1, 2 (auto) or 3 (both persistent kernels)");
             ctx->path_order_pair = (int)value;
         } else if (k == "path_prio") {
             if (value < 0 || value > 256) throw std::runtime_error("path_prio must be in [0, 256]");

@@ -117,7 +117,7 @@ def test_c3_render_tile_subset_bit_exact(c3):
     # NEE runs (shadow rays are traced), though the 1-cm mean free path of the soup occludes the
     # emitter above it from everything the camera sees: the C3 frame is dark by construction
     assert st["shadow_rays"] > 0 and st["extension_rays"] > 0
-    # the cost-ordered pixel fetch (on by default from 64 spp) forced on at 2 spp,
+    # the cost-ordered pixel fetch (on by default from 16 spp) forced on at 2 spp,
     # for k_path and for the deferred form this subset runs with by default
     try:
         for order, defer in ((1, 0), (2, 2)):
@@ -128,7 +128,7 @@ def test_c3_render_tile_subset_bit_exact(c3):
             assert np.array_equal(w2, ow) and np.array_equal(rad2, orad), f"path_order={order} differs"
     finally:
         ctx.set_option("path_order", 2)
-        ctx.set_option("path_order_min_spp", 64)
+        ctx.set_option("path_order_min_spp", 16)
         ctx.set_option("path_defer", 2)
 
 
@@ -148,7 +148,7 @@ def test_c3_full_frame_split_invariance(c3):
                           torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
     finally:
-        ctx.set_option("path_order_min_spp", 64)
+        ctx.set_option("path_order_min_spp", 16)
     packed = film.cpu().numpy()
     assert np.all(packed[3 * n:] == 1.0)
     frame = np.zeros((H, W, 3), np.float32)
@@ -178,7 +178,7 @@ FORMS = [
     ("k_path_defer ordered, paired", dict(path=1, path_defer=1, path_order=2, path_order_pair=1)),
     ("wavefront", dict(path=0, path_defer=2, path_order=2)),
 ]
-DEFAULTS = dict(path=2, path_defer=2, path_order=2, path_order_pair=2, path_order_min_spp=64, count_tests=0,
+DEFAULTS = dict(path=2, path_defer=2, path_order=2, path_order_pair=2, path_order_min_spp=16, count_tests=0,
                 pixel_probe=0)
 
 
