@@ -573,7 +573,12 @@ def test_auto_form_by_shading(hip_ctx_factory):
         cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
         _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
         assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
-        # a small render takes the cost-ordered fetch from path_order_share_min_spp (16) samples
+        # the cost-ordered fetch from path_order_min_spp (16) samples
+        _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
+        assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}
+        # a render of at most path_order_share_pixels pixels takes it from path_order_share_min_spp
+        # (16) samples even when the general floor is higher
+        ctx.set_option("path_order_min_spp", 64)
         _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
         assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}
         ctx.set_option("path_order_share_pixels", 1000)
