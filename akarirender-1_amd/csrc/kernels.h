@@ -4,7 +4,9 @@
 
 namespace akr {
 
-enum : int { TRACE_CLOSEST = 0, TRACE_ANY = 1, TRACE_SHADOW = 2 };
+// TRACE_PILOT: closest-hit traversal that records only each ray's step count (a.ray_steps, capped at
+// a.step_cap) for the cost-ordered fetch's pilot: no hits, no counters
+enum : int { TRACE_CLOSEST = 0, TRACE_ANY = 1, TRACE_SHADOW = 2, TRACE_PILOT = 3 };
 
 // tight = standard slab test (default); !tight = the reference's intersectAABB, bit for bit
 void launch_trace(int mode, bool count, bool tight, bool wide, const TraceArgs &a, uint32_t grid, hipStream_t st);

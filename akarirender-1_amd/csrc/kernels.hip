@@ -502,7 +502,9 @@ __device__ __forceinline__ void trace_exact_lane(const TraceArgs &a, uint32_t id
 #define AKR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(AKR_TRACE_WAVES)))
 template <int MODE, bool COUNT, bool TIGHT, bool WIDE>
 __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs a) {
-    constexpr bool ANY = MODE != TRACE_CLOSEST;  // occlusion query: any hit in (tmin, tmax)
+    constexpr bool ANY = MODE == TRACE_ANY || MODE == TRACE_SHADOW;  // occlusion query: any hit in (tmin, tmax)
+    // the pilot's steps-only build (TRACE_PILOT) counts steps without the counting build's tallies
+    constexpr bool STEPS = COUNT || MODE == TRACE_PILOT;
     __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
@@ -586,8 +588,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                 if (COUNT) {
                     c_strav++;  // every lane of the (converged) wave
                     c_sleaf += busy ? 1 : 0;
-                    steps += busy ? 1 : 0;
                 }
+                if (STEPS) steps += busy ? 1 : 0;
                 if (WIDE && busy && is_internal(cur)) {
                     int nt;
                     if (TIGHT)  // every wide-loop ray of the tight kernel is lean (others: exact lane)
@@ -600,8 +602,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                         c_box += nt;
                         c_visit++;
                         deep = deep || sp > kStackLds;
-                        if (a.step_cap && steps >= a.step_cap) cur = AKR_CHILD_EMPTY;  // pilot: cost capped
                     }
+                    if (STEPS && a.step_cap && steps >= a.step_cap) cur = AKR_CHILD_EMPTY;  // pilot: cost capped
                 } else if (!WIDE && busy && is_internal(cur)) {
                     if (COUNT) {
                         c_box += 2;
@@ -661,10 +663,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                     const float4 ta = k == 0 ? pa : (WIDE && k == 1 ? pa1 : tp[3 * k + 0]);
                     const float4 tb = k == 0 ? pb : (WIDE && k == 1 ? pb1 : tp[3 * k + 1]);
                     const float4 tc = k == 0 ? pc : (WIDE && k == 1 ? pc1 : tp[3 * k + 2]);
-                    if (COUNT) {
-                        c_tri++;
-                        steps++;
-                    }
+                    if (COUNT) c_tri++;
+                    if (STEPS) steps++;
                     float t, u, v;
                     if (mt(o, d, tmin, tmax, ta, tb, tc, ANY ? kInf : best, t, u, v)) {
                         best = t;
@@ -681,8 +681,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             }
             if (busy && ((ANY && occluded) || cur == AKR_CHILD_EMPTY)) {
                 busy = false;
-                emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
-                if (COUNT && a.ray_steps) a.ray_steps[idx] = steps;
+                if constexpr (MODE != TRACE_PILOT) emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
+                if (STEPS && a.ray_steps) a.ray_steps[idx] = steps;
                 if (COUNT) c_deep += deep ? 1 : 0;
             }
         }
@@ -709,8 +709,9 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             }
         }
         if (need_exact) {
-            trace_exact_lane<MODE, TIGHT>(a, idx, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid);
-            if (COUNT && a.ray_steps) a.ray_steps[idx] = 0xFFFFFFFFu;  // traced outside the wide loop
+            if constexpr (MODE != TRACE_PILOT)  // the pilot only ranks such a ray costliest
+                trace_exact_lane<MODE, TIGHT>(a, idx, o, d, invd, tmin, tmax, s_stack, stack_ovf, tid, gtid);
+            if (STEPS && a.ray_steps) a.ray_steps[idx] = 0xFFFFFFFFu;  // traced outside the wide loop
             need_exact = false;
         }
         if (fresh) {
@@ -720,7 +721,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             occluded = false;
             sp = 0;
             leaf = AKR_CHILD_EMPTY;
-            if (COUNT) { c_rays++; c_box++; steps = 0; deep = false; }
+            if (COUNT) { c_rays++; c_box++; deep = false; }
+            if (STEPS) steps = 0;
             const float tr = box_test<TIGHT, WIDE>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, o, invd, tmin, tmax);
             cur = (root == AKR_CHILD_EMPTY || tr < 0.0f || tr > (ANY ? tmax : best)) ? AKR_CHILD_EMPTY : root;
             busy = true;
@@ -2355,8 +2357,12 @@ void launch_trace(int mode, bool count, bool tight, bool wide, const TraceArgs &
     if (wide) {
         if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, true>(count, tight, a, grid, st);
         else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, true>(count, tight, a, grid, st);
-        else launch_trace_mode<TRACE_SHADOW, true>(count, tight, a, grid, st);
+        else if (mode == TRACE_PILOT) {  // steps only: the tight, uncounted wide kernel
+            if (count || !tight) throw std::runtime_error("launch_trace: the pilot mode is tight and uncounted");
+            hipLaunchKernelGGL((k_trace<TRACE_PILOT, false, true, true>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+        } else launch_trace_mode<TRACE_SHADOW, true>(count, tight, a, grid, st);
     } else {
+        if (mode == TRACE_PILOT) throw std::runtime_error("launch_trace: the pilot mode needs the wide view");
         if (mode == TRACE_CLOSEST) launch_trace_mode<TRACE_CLOSEST, false>(count, tight, a, grid, st);
         else if (mode == TRACE_ANY) launch_trace_mode<TRACE_ANY, false>(count, tight, a, grid, st);
         else launch_trace_mode<TRACE_SHADOW, false>(count, tight, a, grid, st);
