@@ -306,6 +306,9 @@ def main():
                     help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
     ap.add_argument("--wavefront-spp", type=int, default=8,
                     help="untimed same-run leg in the wavefront form (north_star's layout), spp; 0 = skip")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearse the N-rank path on a one-GPU box: every rank on device 0, a gloo process group, "
+                         "the frame-end gather through host memory; the line says so and is not a measurement")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -313,7 +316,7 @@ def main():
 
     how, world = launch_plan(args.gpus, os.environ)
     if how == "spawn":
-        sys.exit(spawn_ranks(world, sys.argv[1:], need_devices=not args.launch_check))
+        sys.exit(spawn_ranks(world, sys.argv[1:], need_devices=not (args.launch_check or args.rehearse_one_gpu)))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.launch_check:
@@ -322,16 +325,23 @@ def main():
 
     import torch
     import torch.distributed as dist
-    if world > 1:
+    rehearse = args.rehearse_one_gpu and world > 1
+    if rehearse:   # every rank on device 0; collectives on host tensors over gloo
+        local = 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         if torch.cuda.device_count() <= local:
             raise SystemExit(f"bench.py: rank {rank} needs device {local}, {torch.cuda.device_count()} visible")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world > 1:
         live = dist.get_world_size()   # n_gpus is the live group's size, never a flag
         if live != world:
             raise SystemExit(f"bench.py: launched for {world} ranks, process group has {live}")
         world = live
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if rehearse else dev   # where the collectives run
 
     from akari_amd import capi, scene
 
@@ -400,8 +410,8 @@ def main():
     if world > 1:
         # the frame-end gather once outside the timed region: RCCL connects a collective's channels
         # (ring peers over xGMI) on its first use, which must not land in the timed step
-        gathered = torch.empty(world * film.numel(), device=dev)
-        dist.all_gather_into_tensor(gathered, film)
+        gathered = torch.empty(world * film.numel(), device=cdev)
+        dist.all_gather_into_tensor(gathered, film.to(cdev))
     torch.cuda.synchronize(dev)
 
     # untimed counting pass: traversal tests of one sample pass (algorithmic bytes)
@@ -426,13 +436,13 @@ def main():
     t_start = time.perf_counter()
     ctx.render_device(K, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
     if world > 1:
-        dist.all_gather_into_tensor(gathered, film)     # frame-end gather over RCCL
+        dist.all_gather_into_tensor(gathered, film.to(cdev))     # frame-end gather over RCCL
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     form = ctx.render_form()   # which form the library ran
     if world > 1:
         dist.barrier()
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kstats = ctx.kernel_stats()
@@ -575,7 +585,9 @@ def main():
     line = {
         "metric": {"soup": METRIC, "cornell": METRIC_CORNELL, "hall": METRIC_HALL}[args.scene], "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
         "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f32",
+        "data": ("synthetic; REHEARSAL: the ranks shared one GPU and gathered over gloo, not a measurement"
+                 if rehearse else "synthetic"),
         "config": {"workload": {"soup": "C3 synthetic triangle soup (SURVEY.md §8d)",
                                 "cornell": "C2 Cornell box (reference fixture CornellBox-Original.obj.mesh, SURVEY.md §8d)",
                                 "hall": "C4 stand-in: synthetic textured hall, Diffuse/Glossy/Mix with image textures, "
