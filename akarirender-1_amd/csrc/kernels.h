@@ -30,7 +30,10 @@ void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStre
 void launch_expand_pixels(const uint4 *tiles, uint32_t n_tiles, uint32_t n, uint32_t *pixel, hipStream_t st);
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st);
 // cost-ordered pixel fetch: pilot camera rays, sort keys, and the stable key sort (lbvh.hip, rocPRIM)
-constexpr uint32_t kOrderClassBits = 12, kOrderClassMask = (1u << kOrderClassBits) - 1u;
+// 5-bit cost classes (31 = the costliest, with the rays the pilot does not trace): with the shard's 3 bits
+// the key is one byte, so the radix sort is a single 8-bit pass (12-bit classes took 17 kernel launches,
+// ~0.11 ms; the pilot's 64-step cap at the default shift 2 needs 17 classes)
+constexpr uint32_t kOrderClassBits = 5, kOrderClassMask = (1u << kOrderClassBits) - 1u;
 void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, uint32_t sub, float4 *rays,
                        hipStream_t st);
 void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t sub, uint32_t *key, uint32_t *idx,
