@@ -1968,7 +1968,14 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 
     uint32_t pix = 0, left = 0, seed = 0, pxy = 0;
     V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f};
-    float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
+    // a pixel's film sums live in its (zeroed) film slot, as in k_path: 23 -> 15 VGPRs spilled, time
+    // unchanged; samples close in sample order, so the sums are the sequential ones
+#define DEFER_SPLAT(l)                                 \
+    do {                                               \
+        float4 fm_ = pa.film[pix];                     \
+        splat_one(fm_, (l), pa.ray_clamp);             \
+        pa.film[pix] = fm_;                            \
+    } while (0)
     DeferState s;
     bool need_pixel = true, done = false, fin = false, busy = false;
     uint32_t idle_rounds = 0;    // hang guard: consecutive rounds with no ray in flight in the wave
@@ -2091,7 +2098,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 s.set(DeferState::RUN, 1, 0);
                 s.set(DeferState::LAST, 1, rp);
                 if (s.nsh(rp) == 0 && s.open() == 0)
-                    splat_one(film, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
+                    DEFER_SPLAT(make_float4(Lr.x, Lr.y, Lr.z, 0.0f));
                 else
                     s.set(DeferState::OPEN, 2, s.open() | (1u << rp));
             }
@@ -2111,7 +2118,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         L.y += cc.y;
                         L.z += cc.z;
                     }
-                splat_one(film, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
+                DEFER_SPLAT(make_float4(L.x, L.y, L.z, 0.0f));
                 s.set(DeferState::OPEN, 2, om & ~(1u << q));
                 s.set(DeferState::NSH + 4 * q, 4, 0);
                 atomicAnd(&s_res[tid], ~((0xFFu << (kDeferSlots * q)) | (0xFFu << (16 + kDeferSlots * q))));
@@ -2119,7 +2126,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             // 4. a finished pixel stores its film and fetches the next; free lanes start samples
             const bool free_lane = !busy && !fresh && !want_sh && s.kind() == RAY_NONE;
             if (free_lane && !done && !need_pixel && !s.running() && left == 0 && s.open() == 0) {
-                pa.film[pix] = film;
                 if (pa.probe)
                     pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
                                                COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
@@ -2132,7 +2138,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 pxy = pa.pixel[pix];
                 left = pa.spp;
                 seed = (uint32_t)((int)(pxy & 0xFFFFu) + (int)(pxy >> 16) * pa.cam.width);
-                film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 if (COUNT) pc_closest = pc_shadow = 0;
             }
             try_start(free_lane, fresh, ra, rb);
@@ -2236,6 +2241,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     if (pa.fault_test && pa.fault && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_or(pa.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+#undef DEFER_SPLAT
 
 // Film::merge_tile (core/film.h:85-95) on the device: a context's packed film (one float4 per
 // slot: radiance sums, weight) added into full-frame buffers at its pixels.  `order` (optional)
