@@ -598,7 +598,7 @@ def _tab_fits(cs):
 
 @pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
                                                       (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
-                                                      (1, 1, 1, 1, 0), (1, 1, 1, 1, 2)])
+                                                      (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2)])
 def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab, order):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
     §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
@@ -614,7 +614,8 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
         ctx.set_option("path_order", order)
-        ctx.set_option("path_order_pair", 1 if (order == 2 and defer) else 0)   # paired cost order (§3.10)
+        # paired cost order (§3.10): k_path_defer's (1), or k_path's too (3, an A/B option)
+        ctx.set_option("path_order_pair", (1 if defer else 3) if order == 2 else 0)
         ctx.set_option("path_order_min_spp", 0 if order else 64)
         ctx.set_option("path_order_shift", 0)
     with hip_ctx_factory(0) as ctx:
