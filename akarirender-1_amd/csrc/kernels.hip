@@ -1703,6 +1703,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     uint32_t pix = 0, left = 0, seed = 0;
     int depth = 0;
     V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f};
+    float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
     float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
     bool pend = false;
     bool any = false;           // the lane's ray is a shadow ray (a hit is bgid != kNoHit)
@@ -1801,15 +1802,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             }
             if (COUNT) p_tsh += wall_clock64() - p_ts;
             if (sample_end) {  // Tile::add_sample (core/film.h:66-70), in sample order
-                // the pixel's sums live in its film slot (zeroed by the render's setup), not in four
-                // registers across the loop: two fewer VGPRs spilled, 14 % fewer bytes written per
-                // sample pass
-                {
-                    float4 fm = pa.film[pix];
-                    splat_one(fm, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
-                    pa.film[pix] = fm;
-                }
+                splat_one(film, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
                 if (--left == 0) {
+                    pa.film[pix] = film;
                     if (pa.probe)
                         pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
                                                    COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
@@ -1825,6 +1820,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const uint32_t px = pa.pixel[pix];
                 left = pa.spp;
                 seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 start = true;
                 if (COUNT) pc_closest = pc_shadow = 0;
             }
