@@ -1964,8 +1964,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 
     uint32_t pix = 0, left = 0, seed = 0, pxy = 0;
     V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f};
-    // a pixel's film sums live in its (zeroed) film slot, as in k_path: 23 -> 15 VGPRs spilled, time
-    // unchanged; samples close in sample order, so the sums are the sequential ones
+    // a pixel's film sums live in its (zeroed) film slot, not in registers: 23 -> 15 VGPRs spilled, time
+    // unchanged (the same change made k_path 0.7 % slower, §3.8); samples close in
+    // sample order, so the sums are the sequential ones
 #define DEFER_SPLAT(l)                                 \
     do {                                               \
         float4 fm_ = pa.film[pix];                     \
