@@ -87,7 +87,8 @@ class KernelStat(C.Structure):
 class TraceCounts(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("box_tests", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("per_mode", (C.c_uint64 * 3) * 3),
-                ("lane_slots", (C.c_uint64 * 4) * 3), ("deep_rays", C.c_uint64 * 3)]
+                ("lane_slots", (C.c_uint64 * 4) * 3), ("deep_rays", C.c_uint64 * 3),
+                ("leaf_tests", C.c_uint64 * 3)]
 
 
 class PixelProbe(C.Structure):
@@ -279,6 +280,7 @@ class HipContext:
         self.h = h
         self.device = device
         self._keep = []
+        self._opts = {}   # options set through this object (the library has no getter)
 
     def close(self):
         if getattr(self, "h", None):
@@ -304,6 +306,11 @@ class HipContext:
 
     def set_option(self, key: str, value: int):
         self._check(self.lib.akr_hip_set_option(self.h, key.encode(), int(value)))
+        self._opts[key] = int(value)
+
+    def option_set(self, key: str):
+        """The value this object last set for `key`, or None (the library's default is in effect)."""
+        return self._opts.get(key)
 
     def upload_mesh(self, vertices, indices, normals, texcoords, material_indices, material_slots) -> int:
         v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
@@ -480,7 +487,8 @@ class HipContext:
         modes = ("closest", "any", "shadow")
         per = {m: dict(rays=c.per_mode[k][0], box_tests=c.per_mode[k][1], tri_tests=c.per_mode[k][2],
                        slots_traversal=c.lane_slots[k][0], slots_busy=c.lane_slots[k][1],
-                       slots_tri=c.lane_slots[k][2], visits=c.lane_slots[k][3], deep_rays=c.deep_rays[k])
+                       slots_tri=c.lane_slots[k][2], visits=c.lane_slots[k][3], deep_rays=c.deep_rays[k],
+                       leaf_tests=c.leaf_tests[k])
                for k, m in enumerate(modes)}
         return dict(rays=c.rays, box_tests=c.box_tests, tri_tests=c.tri_tests, per_mode=per)
 

@@ -134,6 +134,7 @@ struct TraceCounters {             // reduced per wave, one atomic per wave
     unsigned long long slots_trav, slots_leaf, slots_tri;  // lane-iterations: traversal loop, busy in it, tri loop
     unsigned long long visits;                             // internal-node visits
     unsigned long long deep;                               // rays whose stack went past kStackLds
+    unsigned long long leaves;                             // leaf records fetched (exact leaf-box tests)
 };
 
 struct TraceArgs {                 // kept small: fewer SGPRs, higher residency

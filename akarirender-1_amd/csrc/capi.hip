@@ -607,14 +607,17 @@ struct akr_hip_ctx {
     // A raised fault word fails the call that sees it (and is cleared): the hang guard of a
     // persistent kernel stopped a wave, so that render's film is incomplete.  Called after the host
     // has waited for a render; a render_device without "verify" reports it at the next call.
-    void check_fault() {
+    void check_fault(const char *which = "the render that raised it") {
         if (!h_fault) return;
         volatile uint32_t *f = reinterpret_cast<volatile uint32_t *>(h_fault);
         if (*f == 0) return;
         *f = 0;
-        throw std::runtime_error("persistent path kernel: a wave stopped on its hang guard; the film of the render "
-                                 "that raised it is incomplete");
+        throw std::runtime_error(std::string("persistent path kernel: a wave stopped on its hang guard; the film of ") +
+                                 which + " is incomplete");
     }
+    // The last render_device ran without "verify" (no host wait): its fault, if any, is found by the
+    // next call, which first waits for that render so the fault is not blamed on its own film.
+    bool unchecked_render = false;
 
     uint32_t grid_for(int mode, uint64_t n) const {
         const uint64_t per_block = (uint64_t)kTraceBlock * (uint64_t)rays_per_lane;
@@ -888,7 +891,11 @@ struct akr_hip_ctx {
         probe_n = 0;
         const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st, look_ok);
         if (N == 0) return 0;
-        check_fault();  // a fault raised by an earlier render_device that ran without "verify"
+        if (unchecked_render) {  // a fault raised by an earlier render_device that ran without "verify"
+            unchecked_render = false;
+            if (done_recorded) HIPCHK(hipEventSynchronize(ev_done));
+            check_fault("the previous render_device call (run without verify; reported by the next render)");
+        }
         uint4 *probe_p = nullptr;  // option "pixel_probe" (not with lookahead lanes)
         if (probe && !cur_look) {
             d_probe.reserve(N);
@@ -1435,13 +1442,60 @@ int akr_hip_upload_lights(akr_hip_ctx *ctx, const akr_area_light *lights, int32_
 }
 
 namespace {
+// An imported tree's triangle records must be this scene's triangles: each record equals the one
+// the builders write for its gid (v0 and the f32 edges v1 - v0, v2 - v0, instance.h:49-50, bit for
+// bit), and every scene triangle is referenced by some leaf.  Shading reads the context's own
+// vertices, so a tree shared from another scene would otherwise render wrong geometry without an
+// error.  O(n_tris) on `n_threads` threads.
+void check_tris_match_mesh(const akr_hip_ctx *ctx, const akr_bvh_tri *tr, uint64_t n, int n_threads) {
+    const uint64_t nt = ctx->n_tris();
+    std::vector<uint8_t> covered(nt, 0);
+    const int T = n_threads > 0 ? std::min(n_threads, 64)
+                                : (int)std::min(64u, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<uint64_t> bad(T, UINT64_MAX);
+    run_on_threads(T, [&](int t) {
+        const uint64_t r0 = n * t / T, r1 = n * (t + 1) / T;
+        for (uint64_t r = r0; r < r1; r++) {
+            const uint32_t g = tr[r].gid;  // < nt: checked by validate_bvh2
+            const float *v0 = &ctx->verts[3 * (size_t)ctx->idx[3 * (size_t)g + 0]];
+            const float *v1 = &ctx->verts[3 * (size_t)ctx->idx[3 * (size_t)g + 1]];
+            const float *v2 = &ctx->verts[3 * (size_t)ctx->idx[3 * (size_t)g + 2]];
+            float want[9];
+            for (int k = 0; k < 3; k++) {
+                want[k] = v0[k];
+                want[3 + k] = v1[k] - v0[k];
+                want[6 + k] = v2[k] - v0[k];
+            }
+            const float got[9] = {tr[r].v0[0], tr[r].v0[1], tr[r].v0[2], tr[r].e1[0], tr[r].e1[1],
+                                  tr[r].e1[2], tr[r].e2[0], tr[r].e2[1], tr[r].e2[2]};
+            if (std::memcmp(want, got, sizeof(want)) != 0) {
+                bad[t] = r;
+                return;
+            }
+            covered[g] = 1;  // racy writes of the same value: fine
+        }
+    });
+    for (uint64_t r : bad)
+        if (r != UINT64_MAX)
+            throw std::runtime_error("imported BVH: triangle record " + std::to_string(r) + " (gid " +
+                                     std::to_string(tr[r].gid) + ") does not match this scene's triangle");
+    for (uint64_t g = 0; g < nt; g++)
+        if (!covered[g])
+            throw std::runtime_error("imported BVH: scene triangle " + std::to_string(g) + " is in no leaf");
+}
+
 // After the BVH2 of ctx->bvh exists (built or imported): the wide view, its device copy, the BVH2
 // itself for the exact lane path, the accel info, and the scene's shading records.
 void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         auto &b = ctx->bvh;
-        build_bvh4(b.nodes, ctx->bvh4, n_threads, ctx->wide_collapse);
-        if (ctx->bvh4.nodes.size() >= kMaxWideNodes)
-            throw std::runtime_error("scene too large: the wide view needs fewer than 2^26 nodes (about 100 M triangles)");
+        ctx->accel_built = false;  // set again only once every buffer below holds the new tree
+        {
+            Bvh4Output w;
+            build_bvh4(b.nodes, w, n_threads, ctx->wide_collapse);
+            if (w.nodes.size() >= kMaxWideNodes)
+                throw std::runtime_error("scene too large: the wide view needs fewer than 2^26 nodes (about 100 M triangles)");
+            ctx->bvh4 = std::move(w);
+        }
         ctx->d_nodes.upload(b.nodes.data(), b.nodes.size(), ctx->stream);
         // Device copy of the wide view: each leaf record is followed by its triangles in one blob, so
         // the leaf phase fetches the exact box and the first triangle in one batch; leaf refs in the
@@ -1517,6 +1571,7 @@ int akr_hip_build_accel(akr_hip_ctx *ctx, const akr_build_params *params) {
         p.intersect_cost = 4.0f;
         if (params) p = *params;
         BvhInput in{ctx->verts.data(), ctx->idx.data(), ctx->n_tris()};
+        ctx->accel_built = false;  // until the new tree is on the device (a failure below leaves none)
         if (p.builder == AKR_BUILDER_LBVH) build_lbvh_gpu(in, ctx->bvh, ctx->stream);
         else if (p.builder == AKR_BUILDER_SAH || p.builder == AKR_BUILDER_SBVH) build_bvh(in, p, ctx->bvh);
         else throw std::runtime_error("unknown builder");
@@ -1535,6 +1590,8 @@ int akr_hip_import_accel(akr_hip_ctx *ctx, const void *nodes, uint64_t n_nodes, 
         const auto *tr = reinterpret_cast<const akr_bvh_tri *>(tris);
         int max_leaf = 0;
         const int depth = validate_bvh2(nd, n_nodes, tr, n_tris, ctx->n_tris(), max_leaf);  // throws on bad input
+        check_tris_match_mesh(ctx, tr, n_tris, n_threads);  // the records are this scene's triangles
+        ctx->accel_built = false;  // until the new tree is on the device (a failure below leaves none)
         BvhOutput &b = ctx->bvh;
         b.nodes.assign(nd, nd + n_nodes);
         b.tris.assign(tr, tr + n_tris);
@@ -1801,6 +1858,7 @@ int akr_hip_render_device(akr_hip_ctx *ctx, const akr_pt_params *params, const a
         ctx->timed("unpack", st, [&] { launch_unpack(ctx->d_film.p, (uint32_t)N, d_radiance, d_weight, st); });
         HIPCHK(hipGetLastError());
         ctx->verify_weights(st, N, params->spp);
+        ctx->unchecked_render = !ctx->verify;
         ctx->mark_done(st);
     });
 }
@@ -1933,6 +1991,7 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out) {
             out->lane_slots[m][2] = c[m].slots_tri;
             out->lane_slots[m][3] = c[m].visits;
             out->deep_rays[m] = c[m].deep;
+            out->leaf_tests[m] = c[m].leaves;
         }
     });
 }

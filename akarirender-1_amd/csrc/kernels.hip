@@ -517,7 +517,8 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const uint32_t root = WIDE ? a.wide_root : nodesu[3].x;
     const float4 *wn = a.wide_nodes;
-    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0, c_visit = 0, c_deep = 0;
+    unsigned long long c_rays = 0, c_box = 0, c_tri = 0, c_strav = 0, c_sleaf = 0, c_stri = 0, c_visit = 0, c_deep = 0,
+                       c_leaf = 0;
     bool deep = false;  // COUNT only: this lane's ray has pushed past the LDS stack
 
     V3 o{0, 0, 0}, d{0, 0, 0}, invd{0, 0, 0};
@@ -648,7 +649,10 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                     pc1 = lr[7];
                     const float tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
                     const bool in = !(tl < 0.0f || tl > (ANY ? tmax : best));
-                    if (COUNT) c_box++;
+                    if (COUNT) {
+                        c_box++;
+                        c_leaf++;
+                    }
                     cnt = in ? fbits(l1.w) : 0u;
                     tp = lr + 2;
                 } else {
@@ -737,6 +741,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
         c_stri = wave_sum(c_stri);
         c_visit = wave_sum(c_visit);
         c_deep = wave_sum(c_deep);
+        c_leaf = wave_sum(c_leaf);
         if (__lane_id() == 0) {
             atomicAdd(&a.counters[MODE].rays, c_rays);
             atomicAdd(&a.counters[MODE].box, c_box);
@@ -746,6 +751,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             atomicAdd(&a.counters[MODE].slots_tri, c_stri);
             atomicAdd(&a.counters[MODE].visits, c_visit);
             atomicAdd(&a.counters[MODE].deep, c_deep);
+            atomicAdd(&a.counters[MODE].leaves, c_leaf);
         }
     }
 }
@@ -1443,7 +1449,8 @@ struct PathRay {
     int sp;
 };
 struct PathCount {
-    unsigned long long rays[2] = {0, 0}, box[2] = {0, 0}, tri[2] = {0, 0}, visit[2] = {0, 0}, deep[2] = {0, 0};
+    unsigned long long rays[2] = {0, 0}, box[2] = {0, 0}, tri[2] = {0, 0}, visit[2] = {0, 0}, deep[2] = {0, 0},
+                       leaf[2] = {0, 0};
     unsigned long long strav = 0, sleaf = 0, stri = 0, iters = 0;
     bool deep_now = false;
 };
@@ -1494,7 +1501,10 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
         const float4 pa1 = lr[5], pb1 = lr[6], pc1 = lr[7];
         const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, r.o, r.invd, r.tmin, r.tmax);
         const bool in = !(tl < 0.0f || tl > r.best);
-        if (COUNT) c.box[kind]++;
+        if (COUNT) {
+            c.box[kind]++;
+            c.leaf[kind]++;
+        }
         const uint32_t cnt = in ? fbits(l1.w) : 0u;
         const float4 *tp = lr + 2;
         for (uint32_t k = 0; k < cnt; k++) {
@@ -1653,7 +1663,7 @@ __device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &
     const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
     for (int m = 0; m < 2; m++) {
         const unsigned long long rr = wave_sum(c.rays[m]), b = wave_sum(c.box[m]), t = wave_sum(c.tri[m]),
-                                 v = wave_sum(c.visit[m]), dp = wave_sum(c.deep[m]);
+                                 v = wave_sum(c.visit[m]), dp = wave_sum(c.deep[m]), lf = wave_sum(c.leaf[m]);
         if (__lane_id() == 0) {
             TraceCounters &tc = a.counters[slot_of[m]];
             atomicAdd(&tc.rays, rr);
@@ -1661,6 +1671,7 @@ __device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &
             atomicAdd(&tc.tri, t);
             atomicAdd(&tc.visits, v);
             atomicAdd(&tc.deep, dp);
+            atomicAdd(&tc.leaves, lf);
         }
     }
     // lane-slot utilisation of the shared loop: under the closest-hit set

@@ -4,9 +4,13 @@ The render form is the library's choice (the persistent path ke
 config.form names it, and an untimed same-run leg reports north_star's wavefront layout beside it
 (wavefront_ms_per_step).
 
-A step is one sample per pixel over the whole frame (2,073,600 path samples).  K steps are one
-render(spp=K) call per rank over that rank's tiles; the frame-end gather to rank 0 (RCCL via
-torch.distributed) is inside the timed region.  value = W*H*K / max-over-ranks time.
+A step is spp_per_step = ceil(--frame-spp / K) samples per pixel over the whole frame, so the K timed
+steps render the metric's 1024-spp frame (--frame-spp, default 1024; the driver's --steps 20 renders
+20 x 52 = 1040 spp).  The K steps are one render(spp = K * spp_per_step) call per rank over that rank's
+tiles: a pixel's samples are one sequential chain through its sampler stream (cpu/integrator.cpp:
+124-134), so the frame cannot be cut into independent per-step renders without repeating samples.
+The frame-end gather to rank 0 (RCCL via torch.distributed) is inside the timed region.
+value = W*H*K*spp_per_step / max-over-ranks time.
 
 Launch: python bench.py [--gpus N --steps K --warmup W].  Under torch.distributed.run (WORLD_SIZE set)
 each process is one rank and --gpus must equal the world size.  Without it, --gpus N > 1 starts the N
@@ -33,6 +37,8 @@ METRIC = "Msamples/sec (whole node), 10M-tri scene 1080p 1024spp, 1/2/4/8 MI355X
 METRIC_CORNELL = "Msamples/sec, Cornell box 1080p 1024spp, 1x MI355X (BASELINE.json configs[1])"
 METRIC_HALL = "Msamples/sec, Sponza-class textured scene 4K (BASELINE.json configs[3] stand-in), 1x MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCDs
+SCLK_HZ = 2.4e9                # MI355X shader clock (MI355X_MICROARCH.md: "120 cycles at 2.4 GHz")
 RAY_BYTES, BOX_BYTES, TRI_BYTES = 32, 32, 40   # SURVEY.md §8d algorithmic bytes per ray / AABB / triangle test
 
 
@@ -46,34 +52,77 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def measured_traffic(kernel, workload, per_spp=None):
-    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this same workload
-    (profiles/<tag>_traffic.json, written by tools/prof_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE rocprofv3 passes, gfx950 FETCH_SIZE x2 correction).  PMC passes cannot run inside
-    the timed region, so the figure is the profile's; (None, None) when no profile matches."""
+def measured_traffic(kernel, workload, spp=None, profiles_dir=None):
+    """The PMC record of `kernel` from the newest committed profile of this exact workload
+    (profiles/<tag>_traffic.json, written by tools/prof_summary.py from separate rocprofv3 passes of
+    tools/profile_driver.sh, gfx950 FETCH_SIZE x2 correction).  A profile matches only when its
+    workload equals the line's `config` field for field, so a 1-spp, unordered or whole-frame
+    profile never stands in for a 1040-spp ordered launch or a rank's share.  PMC passes cannot run
+    inside the timed region, so the figures are the profile's.  Returns (record, source) with
+    `traffic` = HBM bytes of one launch (a persistent launch: per-spp bytes x `spp`), or (None, None)."""
     best = None
-    for p in sorted((ROOT / "profiles").glob("*_traffic.json")):
+    names = [kernel] if isinstance(kernel, str) else list(kernel)
+    for p in sorted(Path(profiles_dir or ROOT / "profiles").glob("*_traffic.json")):
         try:
             d = json.loads(p.read_text())
         except (OSError, ValueError):
             continue
         w = d.get("workload") or {}
-        defaults = {"builder": "sah"}  # profiles written before the key existed
-        names = [kernel] if isinstance(kernel, str) else list(kernel)
         name = next((k for k in names if k in d.get("kernels", {})), None)
-        if any(w.get(k, defaults.get(k)) != v for k, v in workload.items()) or name is None:
+        if name is None or any(w.get(k) != v for k, v in workload.items()) or set(w) - set(workload):
             continue
-        rec = d["kernels"][name]
-        if per_spp is not None:   # a persistent launch renders every spp: scale the profile's per-spp bytes
+        rec = dict(d["kernels"][name])
+        if spp is not None:   # a persistent launch renders every spp: scale the profile's per-spp bytes
             if "hbm_bytes_per_spp" not in rec:
                 continue
-            best = (rec["hbm_bytes_per_spp"] * per_spp, f"profiles/{p.name}")
+            rec["traffic"] = rec["hbm_bytes_per_spp"] * spp
+            if "l2_req_bytes_per_spp" in rec:
+                rec["l2_bytes"] = rec["l2_req_bytes_per_spp"] * spp
         else:
-            best = (rec["hbm_bytes_per_launch"], f"profiles/{p.name}")
+            if "hbm_bytes_per_launch" not in rec:
+                continue
+            rec["traffic"] = rec["hbm_bytes_per_launch"]
+            if "l2_req_bytes_per_launch" in rec:
+                rec["l2_bytes"] = rec["l2_req_bytes_per_launch"]
+        best = (rec, f"profiles/{p.name}")
     return best if best else (None, None)
 
 
-from akari_amd.dist import tiles_for_rank  # noqa: E402  (interleaved tile k -> rank k % world)
+def latency_model(prof, cl, sh, npix, samples_per_s):
+    """A ceiling for the latency-bound path kernel that does not saturate.
+    Every ray is a chain of dependent fetches: the root box, one wide node per visit, one leaf
+    record per leaf test (counted by the instrumented pass).  If each of the launch's resident lanes
+    always had exactly one such fetch in flight and did nothing else, the launch would finish
+    lanes / (rounds per sample x fetch latency) samples per second (Little's law), with the
+    fetch latency the PMC pass's mean VMEM issue-to-return time (VmemLatency, cycles at SCLK_HZ).
+    `frac` = achieved / that ceiling: the share of lane-time the chains actually spend waiting on
+    their own next fetch.  It rises when lanes idle less (fuller waves, fewer processing phases) and
+    falls when a change only shortens the latency the achieved rate is divided by."""
+    c = prof.get("counters", {})
+    lat = c.get("VmemLatency")
+    lanes = prof.get("grid_threads")
+    if not lat or not lanes:
+        return None
+    rounds = (cl["rays"] + cl["visits"] + cl["leaf_tests"] + sh["rays"] + sh["visits"] + sh["leaf_tests"]) / max(1, npix)
+    lat_s = lat / SCLK_HZ
+    ceiling = lanes / (rounds * lat_s)
+    out = {"vmem_latency_cycles": round(lat, 1), "dependent_rounds_per_sample": round(rounds, 2),
+           "resident_lanes": lanes, "ceiling_samples_per_s": round(ceiling, 1),
+           "frac": round(samples_per_s / ceiling, 4)}
+    if c.get("TCP_TCC_READ_REQ_sum"):
+        out["l1_to_l2_read_latency_cycles"] = round(c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"], 1)
+    if c.get("TCC_EA0_RDREQ_sum"):
+        out["l2_to_fabric_read_latency_cycles"] = round(c["TCC_EA0_RDREQ_LEVEL_sum"] / c["TCC_EA0_RDREQ_sum"], 1)
+    if c.get("SQ_WAVE_CYCLES"):
+        wc = c["SQ_WAVE_CYCLES"]
+        out["wave_time"] = {"parked_waitcnt": round(c["SQ_WAIT_ANY"] / wc, 4),
+                            "issue_stalled": round(c["SQ_WAIT_INST_ANY"] / wc, 4),
+                            "issuing": round(c["SQ_ACTIVE_INST_ANY"] / wc, 4),
+                            "valu_active": round(c["SQ_ACTIVE_INST_VALU"] / wc, 4)}
+    return out
+
+
+from akari_amd.dist import tile_grid, tiles_for_rank, unpack_to_frame  # noqa: E402  (tile k -> rank k % world)
 
 
 def host_cpus() -> dict:
@@ -264,9 +313,11 @@ def main():
                          "starts the ranks itself")
     ap.add_argument("--launch-check", action="store_true",
                     help="test the rank launch and the frame-end gather on CPU (gloo), no GPU work")
-    ap.add_argument("--steps", type=int, default=1024,
-                    help="spp of the timed render (default: the metric's 1024-spp frame, ~6 s at N = 1)")
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed steps K; a step renders ceil(--frame-spp / K) spp of the whole frame")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed steps before the timed region (one render)")
+    ap.add_argument("--frame-spp", type=int, default=1024,
+                    help="spp the K timed steps render together at least (the metric's 1024-spp frame)")
     ap.add_argument("--scene", choices=["soup", "cornell", "hall"], default="soup",
                     help="soup: C3, the headline workload; cornell: C2 (BASELINE.json configs[1], the reference's "
                          "Cornell box at 1080p on one GPU); hall: C4 stand-in (configs[3], a synthetic textured hall "
@@ -309,6 +360,9 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearse the N-rank path on a one-GPU box: every rank on device 0, a gloo process group, "
                          "the frame-end gather through host memory; the line says so and is not a measurement")
+    ap.add_argument("--verify-frame", action="store_true",
+                    help="N > 1: rank 0 assembles the gathered frame and checks it bit for bit against a single "
+                         "whole-frame render of its own context (after the timed region; tests)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="single-process scaling probe: render only rank 0's tiles of an N-rank split "
                          "(prints the per-rank time; not a bench line for the driver)")
@@ -348,6 +402,10 @@ def main():
     W = args.width or (3840 if args.scene == "hall" else 1920)
     H = args.height or (2160 if args.scene == "hall" else 1080)
     K, Wm = args.steps, args.warmup
+    if K < 1:
+        raise SystemExit("bench.py: --steps must be >= 1")
+    sps = max(1, -(-args.frame_spp // K))   # spp per step: K steps render >= --frame-spp spp
+    spp = K * sps                           # the timed render's spp
     t0 = time.time()
     if args.scene == "cornell":
         sc = scene.cornell_scene(ROOT / "tests" / "golden" / "CornellBox-Original.obj.mesh", resolution=(W, H))
@@ -405,7 +463,7 @@ def main():
 
     # warmup (also JIT/cache warm)
     if Wm > 0:
-        ctx.render_device(Wm, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+        ctx.render_device(Wm * sps, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
     gathered = None
     if world > 1:
         # the frame-end gather once outside the timed region: RCCL connects a collective's channels
@@ -434,7 +492,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    ctx.render_device(K, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+    ctx.render_device(spp, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
     if world > 1:
         dist.all_gather_into_tensor(gathered, film.to(cdev))     # frame-end gather over RCCL
     torch.cuda.synchronize(dev)
@@ -445,14 +503,32 @@ def main():
         tt = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    frame_check = None
+    if args.verify_frame and world > 1:
+        # the gathered films (the timed render's) assembled into the frame on rank 0 and compared
+        # with one whole-frame render of rank 0's own context; every rank reports whether it adopted
+        # rank 0's BVH (akr_hip_import_accel leaves build_ms 0) instead of building its own
+        adopted = [None] * world
+        dist.all_gather_object(adopted, bool(rank != 0 and info.build_ms == 0.0))
+        if rank == 0:
+            parts = gathered.cpu().numpy().reshape(world, -1)
+            frad = np.zeros((H, W, 3), np.float32)
+            fw = np.zeros((H, W), np.float32)
+            for r in range(world):
+                unpack_to_frame(parts[r], tiles_for_rank(W, H, args.tile, r, world), W, H, frad, fw)
+            rrad, rw = ctx.render(spp, args.max_depth, tile_grid(W, H, args.tile), W, H)
+            frame_check = {"bit_exact": bool(frad.tobytes() == rrad.tobytes() and fw.tobytes() == rw.tobytes()),
+                           "max_abs_diff": float(np.abs(frad - rrad).max()), "weights_equal": bool(np.array_equal(fw, rw)),
+                           "mean_radiance": float(rrad.mean() / max(1, spp)), "adopted_bvh": adopted,
+                           "reference": "one whole-frame akr_hip_render of rank 0's context"}
     kstats = ctx.kernel_stats()
     la = ctx.render_info()
-    # sanity: every pixel of this rank got K samples
-    assert int(wgt[:npix].min().item()) == K and int(wgt[:npix].max().item()) == K
-    # untimed per-kernel breakdown (events on every launch) over a few more steps
+    # sanity: every pixel of this rank got every sample of the timed render
+    assert int(wgt[:npix].min().item()) == spp and int(wgt[:npix].max().item()) == spp
+    # untimed per-kernel breakdown (events on every launch) over a few more samples
     ctx.reset_stats()
     ctx.set_option("stats", 1)
-    ctx.render_device(min(K, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+    ctx.render_device(min(spp, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
     torch.cuda.synchronize(dev)
     bstats = ctx.kernel_stats()
     # wavefront form: the shadow trace timed alone (on the main stream, not overlapping the
@@ -461,7 +537,7 @@ def main():
     if "trace_shadow" in bstats:
         ctx.reset_stats()
         ctx.set_option("serial_shadow", 1)
-        ctx.render_device(min(K, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+        ctx.render_device(min(spp, 4), args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
         torch.cuda.synchronize(dev)
         iso = ctx.kernel_stats()
         ctx.set_option("serial_shadow", 0)
@@ -469,19 +545,26 @@ def main():
     # -> splat launches per bounce), when the timed render ran a persistent kernel
     wavefront = None
     if rank == 0 and args.wavefront_spp > 0 and form["form"] in ("k_path", "k_path_defer"):
+        # the plain wavefront (no lookahead lanes), whatever options the timed render ran with;
+        # the options in effect before are restored afterwards
+        saved = {k: ctx.option_set(k) for k in ("stats", "path", "lookahead")}
         ctx.reset_stats()
         ctx.set_option("stats", 0)
         ctx.set_option("path", 0)
+        ctx.set_option("lookahead", 1)
         ctx.render_device(1, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)   # warm
         torch.cuda.synchronize(dev)
         tw = time.perf_counter()
         ctx.render_device(args.wavefront_spp, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
         torch.cuda.synchronize(dev)
         tw = time.perf_counter() - tw
-        assert ctx.render_form()["form"] == "wavefront"
-        ctx.set_option("path", args.path)
-        wavefront = {"ms_per_step": round(tw / args.wavefront_spp * 1e3, 3), "spp": args.wavefront_spp,
-                     "Msamples_per_s": round(npix * args.wavefront_spp / tw / 1e6, 3), "timed": False}
+        wform = ctx.render_form()["form"]
+        for k, v in saved.items():
+            if v is not None:   # every one of them was set above (bench options / --opt)
+                ctx.set_option(k, v)
+        wavefront = {"ms_per_spp": round(tw / args.wavefront_spp * 1e3, 3), "spp": args.wavefront_spp,
+                     "form": wform, "Msamples_per_s": round(npix * args.wavefront_spp / tw / 1e6, 3),
+                     "timed": False}
 
     if rank != 0:
         if world > 1:
@@ -490,9 +573,9 @@ def main():
 
     if split != world:  # scaling probe: one rank's share of an N-way split, on this GPU
         print(json.dumps({"probe": "emulated rank 0 of a tile split", "emulate_world": split, "rank_pixels": npix,
-                          "rank_ms_per_step": round(elapsed / K * 1e3, 3),
-                          "rank_Msamples_per_s": round(npix * K / elapsed / 1e6, 3), "lookahead": la,
-                          "projected_node_Msamples_per_s": round(W * H * K / elapsed / 1e6, 3),
+                          "spp": spp, "rank_ms_per_spp": round(elapsed / spp * 1e3, 4),
+                          "rank_Msamples_per_s": round(npix * spp / elapsed / 1e6, 3), "lookahead": la,
+                          "projected_node_Msamples_per_s": round(W * H * spp / elapsed / 1e6, 3),
                           "form": form, "wavefront": wavefront,
                           "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                                       for k, v in bstats.items()},
@@ -500,16 +583,26 @@ def main():
                                              "shadow": counts["per_mode"]["shadow"]["rays"] / max(1, npix)}}),
               flush=True)
         return
-    samples = W * H * K
+    samples = W * H * spp
     value = samples / elapsed / 1e6
+    config = {"workload": {"soup": "C3 synthetic triangle soup (SURVEY.md §8d)",
+                           "cornell": "C2 Cornell box (reference fixture CornellBox-Original.obj.mesh, SURVEY.md §8d)",
+                           "hall": "C4 stand-in: synthetic textured hall, Diffuse/Glossy/Mix with image textures, "
+                                   "area lights (scene.hall_scene)"}[args.scene], "triangles": cs.n_tris,
+              "width": W, "height": H, "spp_per_step": sps, "spp": spp, "max_depth": args.max_depth,
+              "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
+              "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la,
+              # the form the library ran (north_star names a wavefront; DESIGN.md §0 / §3.8 give the
+              # measured reason for the persistent kernel on this scene) and the wavefront beside it
+              "form": form["form"], "ordered_fetch": form["ordered"]}
     # roofline of the dominant kernel: the persistent path kernel (every closest-hit and shadow ray
     # of the render, SURVEY.md §8d "t_traversal_kernels"), or the wavefront's closest-hit trace
     cl = counts["per_mode"]["closest"]
     sh = counts["per_mode"]["shadow"]
     ray_bytes = lambda c: RAY_BYTES * c["rays"] + BOX_BYTES * c["box_tests"] + TRI_BYTES * c["tri_tests"]
     dom = "path" if "path" in cstats else "trace_closest"
-    if dom == "path":   # the counting pass rendered 1 spp; the timed launch renders K
-        bytes_per_launch = (ray_bytes(cl) + ray_bytes(sh)) * K
+    if dom == "path":   # the counting pass rendered 1 spp; the timed launch renders spp
+        bytes_per_launch = (ray_bytes(cl) + ray_bytes(sh)) * spp
         prof_name = PATH_KERNEL_PROF_NAME
     else:
         bytes_per_launch = ray_bytes(cl) / (cstats.get("trace_closest", {}).get("launches", 0) or 1)
@@ -517,22 +610,31 @@ def main():
     kc = kstats.get(dom) or bstats[dom]   # timed region (breakdown pass if --timed-stats 0)
     avg_ms = kc["total_ms"] / kc["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = measured_traffic(prof_name, {
-        "triangles": cs.n_tris, "width": W, "height": H, "max_depth": args.max_depth, "bvh_leaf": args.leaf,
-        "sah_isect": args.sah_isect, "builder": args.builder}, per_spp=K if dom == "path" else None)
-    # hardware fraction beside the model one: the PMC-measured HBM bytes of the same kernel (committed
-    # profile of this workload) over the live launch time
+    # the PMC record of the same kernel from the committed profile of this exact config (the driver's
+    # command, tools/profile_driver.sh); None when no profile of this config exists
+    prof, traffic_src = measured_traffic(prof_name, config, spp=spp if dom == "path" else None)
+    traffic = prof["traffic"] if prof else None
+    # hardware fraction beside the model one: the PMC-measured HBM bytes over the live launch time
     hbm_achieved = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
+    l2_bytes = prof.get("l2_bytes") if prof else None
+    l2_achieved = l2_bytes / (avg_ms * 1e-3) / 1e9 if l2_bytes else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "hbm_achieved": round(hbm_achieved, 1) if hbm_achieved else None,
                 "hbm_frac": round(hbm_achieved / HBM_PEAK_GBS, 4) if hbm_achieved else None,
+                # L2 request bandwidth of the same launch (TCC_REQ x 128 B, PMC) against the L2 peak
+                "l2_achieved": round(l2_achieved, 1) if l2_achieved else None,
+                "l2_peak": L2_PEAK_GBS,
+                "l2_frac": round(l2_achieved / L2_PEAK_GBS, 4) if l2_achieved else None,
                 "rays_per_sample": {"closest": cl["rays"] / max(1, npix), "shadow": sh["rays"] / max(1, npix)},
                 "kernel": dom, "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
                 "per_ray": {"box_tests": cl["box_tests"] / max(1, cl["rays"]),
                             "node_visits": cl["visits"] / max(1, cl["rays"]),
+                            "leaf_tests": cl["leaf_tests"] / max(1, cl["rays"]),
                             "tri_tests": cl["tri_tests"] / max(1, cl["rays"])},
                 "shadow_per_ray": {"box_tests": sh["box_tests"] / max(1, sh["rays"]),
+                                   "node_visits": sh["visits"] / max(1, sh["rays"]),
+                                   "leaf_tests": sh["leaf_tests"] / max(1, sh["rays"]),
                                    "tri_tests": sh["tri_tests"] / max(1, sh["rays"])},
                 # SIMD lane utilisation of the traversal loop (node visits per lane slot) and of
                 # the triangle loop (triangle tests per lane slot), from the counting pass; the path
@@ -545,7 +647,8 @@ def main():
                                    "holding_ray": c["slots_busy"] / max(1, c["slots_traversal"]),
                                    "triangles": c["tri_tests"] / max(1, c["slots_tri"])}
                                for m, c in (("closest", cl), ("shadow", sh))})}
-
+    if dom == "path" and prof:
+        roofline["latency"] = latency_model(prof, cl, sh, npix, value * 1e6)
     if achieved > HBM_PEAK_GBS:   # the model bytes are not HBM bytes: caches serve most of them
         roofline["note"] = ("the SURVEY.md §8d algorithmic bytes exceed the HBM peak: most node and triangle reads "
                             "hit L2 or the Infinity Cache (on C3 ~73 % L2 hits by PMC; a small scene's BVH is wholly "
@@ -584,23 +687,15 @@ def main():
 
     line = {
         "metric": {"soup": METRIC, "cornell": METRIC_CORNELL, "hall": METRIC_HALL}[args.scene], "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
-        "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "ms_per_step": round(elapsed / K * 1e3, 3), "ms_per_spp": round(elapsed / spp * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32",
         "data": ("synthetic; REHEARSAL: the ranks shared one GPU and gathered over gloo, not a measurement"
                  if rehearse else "synthetic"),
-        "config": {"workload": {"soup": "C3 synthetic triangle soup (SURVEY.md §8d)",
-                                "cornell": "C2 Cornell box (reference fixture CornellBox-Original.obj.mesh, SURVEY.md §8d)",
-                                "hall": "C4 stand-in: synthetic textured hall, Diffuse/Glossy/Mix with image textures, "
-                                        "area lights (scene.hall_scene)"}[args.scene], "triangles": cs.n_tris,
-                   "width": W, "height": H, "spp_per_step": 1, "max_depth": args.max_depth,
-                   "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
-                   "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la,
-                   # the form the library ran (north_star names a wavefront; DESIGN.md §0 / §3.8 give the
-                   # measured reason for the persistent kernel on this scene) and the wavefront beside it
-                   "form": form["form"], "ordered_fetch": form["ordered"]},
-        "wavefront_ms_per_step": wavefront["ms_per_step"] if wavefront else None,
+        "config": config,
+        "wavefront_ms_per_spp": wavefront["ms_per_spp"] if wavefront else None,
         "wavefront": wavefront,
-        "roofline": roofline, "cpu_baseline": cpu,
+        "roofline": roofline, "cpu_baseline": cpu, "frame_check": frame_check,
         # per-kernel averages from an untimed pass with events on every launch (the timed region
         # times trace_closest only: events around every launch cost ~7 % at an 8-way rank)
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}

@@ -46,8 +46,9 @@
 extern "C" {
 #endif
 
-/* 2: akr_trace_counts gained deep_rays[3]; akr_pixel_probe / akr_hip_pixel_probe added */
-#define AKR_HIP_API_VERSION 2
+/* 2: akr_trace_counts gained deep_rays[3]; akr_pixel_probe / akr_hip_pixel_probe added
+ * 3: akr_trace_counts gained leaf_tests[3] */
+#define AKR_HIP_API_VERSION 3
 
 typedef struct akr_hip_ctx akr_hip_ctx;
 
@@ -180,6 +181,9 @@ typedef struct akr_trace_counts {
     /* rays per mode whose traversal stack grew past the LDS-resident entries into the global
      * overflow area (the deep-stack path, kernels.hip stack_pop / wide_order_push) */
     uint64_t deep_rays[3];
+    /* leaf records fetched per mode (each an exact leaf-box test; with the node visits, the
+     * dependent fetch rounds of a traversal) */
+    uint64_t leaf_tests[3];
 } akr_trace_counts;
 
 /* Test-only per-pixel fingerprint of the last render's sample loop (option "pixel_probe" = 1),

@@ -49,18 +49,31 @@ def test_gpus_beyond_visible_devices_fails_loudly():
     assert "needs 2 visible GPUs" in r.stderr
 
 
-def test_roofline_traffic_from_the_newest_matching_profile():
-    """roofline.traffic is the PMC HBM bytes of the dominant kernel from the newest committed profile
-    of the same workload, looked up under every rocprof name the kernel has had."""
-    c3 = {"triangles": 10_000_002, "width": 1920, "height": 1080, "max_depth": 5, "bvh_leaf": 4, "sah_isect": 4.0,
-          "builder": "sbvh"}
-    t, src = bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, c3, per_spp=1024)
-    newest = sorted((ROOT / "profiles").glob("*_traffic.json"))[-1].name
-    assert src == f"profiles/{newest}" and t is not None and t > 0
-    per_spp = json.loads((ROOT / src).read_text())["kernels"]["k_path<false, true>"]["hbm_bytes_per_spp"]
-    assert t == per_spp * 1024
-    # another workload matches nothing
-    assert bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, dict(c3, triangles=5), per_spp=1) == (None, None)
+def test_roofline_traffic_only_from_a_profile_of_the_same_config(tmp_path):
+    """roofline.traffic / l2 / latency come from the newest committed PMC profile whose workload is
+    the line's config field for field: a 1-spp, unordered or whole-frame profile
+    never stands in for the timed 1040-spp ordered launch or a rank's share."""
+    cfg = {"workload": "C3", "triangles": 10_000_002, "width": 1920, "height": 1080, "spp_per_step": 52,
+           "spp": 1040, "form": "k_path", "ordered_fetch": True, "parallelism": "tile-split x1",
+           "lookahead": {"lanes": 1, "passes": 1}}
+    rec = {"hbm_bytes_per_spp": 11.5e9, "l2_req_bytes_per_spp": 40e9, "counters": {"VmemLatency": 900.0},
+           "grid_threads": 262144}
+    for tag, w in (("r01", cfg), ("r02", dict(cfg, ordered_fetch=False)), ("r03", dict(cfg, spp=20)),
+                   ("r04", dict(cfg, extra=1))):
+        (tmp_path / f"{tag}_traffic.json").write_text(json.dumps({"workload": w, "kernels": {"k_path<false, true>": rec}}))
+    prof, src = bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, cfg, spp=1040, profiles_dir=tmp_path)
+    assert src == "profiles/r01_traffic.json"
+    assert prof["traffic"] == 11.5e9 * 1040 and prof["l2_bytes"] == 40e9 * 1040
+    # a rank share, an unordered launch or another spp matches nothing
+    for other in (dict(cfg, parallelism="tile-split x8"), dict(cfg, ordered_fetch=False, spp=7), dict(cfg, triangles=5)):
+        assert bench.measured_traffic(bench.PATH_KERNEL_PROF_NAME, other, spp=1040, profiles_dir=tmp_path) == (None, None)
+    # the latency model of the line
+    cl = {"rays": 4, "visits": 100, "leaf_tests": 20}
+    sh = {"rays": 1, "visits": 20, "leaf_tests": 5}
+    lat = bench.latency_model(prof, cl, sh, 1, 1e9)
+    assert lat["dependent_rounds_per_sample"] == 150
+    assert abs(lat["ceiling_samples_per_s"] - 262144 / (150 * 900 / bench.SCLK_HZ)) < 1
+    assert 0 < lat["frac"] < 1
 
 
 def test_visible_gpu_count_from_sysfs(tmp_path):

@@ -373,6 +373,18 @@ def test_import_accel_bit_exact(hip_ctx_factory):
         bad[3]["child"][0] = len(nodes) + 10
         with pytest.raises(capi.AkrError, match="BVH"):
             b.import_accel(bad, tris)
+        # records that are not this scene's triangles, or a scene triangle in no leaf
+        moved = tris.copy()
+        moved[5]["v0"][1] += 1e-3
+        with pytest.raises(capi.AkrError, match="does not match"):
+            b.import_accel(nodes, moved)
+        relabelled = tris.copy()
+        g = relabelled["gid"]
+        relabelled["gid"] = np.where(g == g[0], g[1], g)   # triangle g[0] vanishes from every leaf
+        with pytest.raises(capi.AkrError, match="does not match|in no leaf"):
+            b.import_accel(nodes, relabelled)
+        # a refused import leaves the previous tree in place, consistent with the device
+        _check_render(b, orc, 1, 5, [(0, 0, 64, 36)], 64, 36)
 
 
 def test_hang_guard_fault_is_reported(hip_ctx_factory):
@@ -397,6 +409,12 @@ def test_hang_guard_fault_is_reported(hip_ctx_factory):
         ctx.render_device(2, 5, tiles, rad.data_ptr(), wt.data_ptr())
         with pytest.raises(capi.AkrError, match="hang guard"):
             ctx.synchronize()
+        # an unverified render's fault found by the next render names the earlier call
+        ctx.render_device(2, 5, tiles, rad.data_ptr(), wt.data_ptr())
+        ctx.set_option("fault_test", 0)
+        with pytest.raises(capi.AkrError, match="previous render_device"):
+            ctx.render_device(2, 5, tiles, rad.data_ptr(), wt.data_ptr())
+        ctx.set_option("fault_test", 1)
         ctx.set_option("verify", 1)
         ctx.set_option("fault_test", 0)
         _check_render(ctx, orc, 2, 5, tiles, 32, 32)

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(capi.EXPORTS) == declared, "ctypes binding out of sync with include/akr_hip.h"
-    assert capi.load_library().akr_hip_api_version() == 2
+    assert capi.load_library().akr_hip_api_version() == 3
 
 
 def test_tile_arrays_pass_without_copy():

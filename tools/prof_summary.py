@@ -1,10 +1,16 @@
-"""Summarise a tools/profile.sh run (rocprofv3 csv) into profiles/<tag>_summary.md + copies of the
-kernel stats / counter csvs.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and
-reads half the bytes of 128-byte-line traffic on gfx950, so traffic = 2 * FETCH_SIZE * 1024; the
-TCC_MISS_sum * 128 B column is printed beside it as the calibration check for this access pattern.
-WRITE_SIZE (KiB, exact for 16-B-per-lane stores and float atomics per the guide) is added unscaled.
-Also writes profiles/<tag>_traffic.json: HBM bytes per launch per kernel, which bench.py reports as
-roofline.traffic when the workload matches."""
+"""Summarise a tools/profile_driver.sh (or tools/profile.sh) run (rocprofv3 csv) into
+profiles/<tag>_summary.md, profiles/<tag>_traffic.json and copies of the kernel stats / counter csvs.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and reads half the bytes of
+128-byte-line traffic on gfx950, so read traffic = 2 * FETCH_SIZE * 1024; WRITE_SIZE (KiB) is added
+unscaled; TCC_MISS * 128 B is printed beside it as the calibration check for this access pattern.
+
+The persistent path kernel renders every spp of its call in one launch, and bench.py launches it
+for the warmup, the timed render and an untimed breakdown.  Its record in traffic.json is the
+*timed* launch alone: the longest dispatch of that kernel in each pass (the timed render has the
+most spp), with `spp` from the bench line (steps x spp_per_step) and every counter of that one
+dispatch, so bench.py's roofline reads the launch the driver times.  The
+workload key is the bench line's whole `config`, which bench.py matches field for field."""
 import csv
 import json
 import shutil
@@ -13,6 +19,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
+PASSES = ("fetch", "write", "tcc", "sq", "lat", "ea", "pmc_fetch", "pmc_write", "pmc_tcc")
 
 
 def short(name):
@@ -20,11 +27,39 @@ def short(name):
     return name.split("(")[0]
 
 
+def bench_line(log: Path):
+    if not log.exists():
+        return None
+    lines = [l for l in log.read_text().splitlines() if l.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
+def read_pass(f: Path):
+    """{kernel: {dispatch_id: {"dur_ns": ..., counters...}}} of one PMC pass csv."""
+    out = defaultdict(dict)
+    meta = {}
+    for r in csv.DictReader(open(f)):
+        if "akr::" not in r["Kernel_Name"]:
+            continue
+        k = short(r["Kernel_Name"])
+        d = out[k].setdefault(int(r["Dispatch_Id"]), {"dur_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        meta[k] = (r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"], r["Scratch_Size"],
+                   r["Grid_Size"])
+    return out, meta
+
+
+def is_path_kernel(k):   # the uncounted persistent path kernels (k_path<false, ...>, k_path_defer<false, ...>)
+    return k.startswith("k_path") and "<true" not in k
+
+
 def main(tag):
     src = ROOT / "gpurun_out" / f"prof_{tag}"
     dst = ROOT / "profiles"
     dst.mkdir(exist_ok=True)
-    out = [f"# rocprofv3 summary — {tag}", "", f"Command: `tools/profile.sh {tag}` (see tools/profile.sh).", ""]
+    args = (src / "args.txt").read_text().strip() if (src / "args.txt").exists() else "(tools/profile.sh)"
+    out = [f"# rocprofv3 summary — {tag}", "", f"Command: `python3 bench.py {args}` under rocprofv3 "
+           f"(`tools/profile_driver.sh {tag}`: one pass per counter group, `--kernel-trace` only beside them).", ""]
     ks = list(csv.DictReader(open(src / "kt" / "run_kernel_stats.csv")))
     out += ["## Kernel time (`rocprofv3 --kernel-trace --stats`)", "",
             "| kernel | calls | total ms | avg ms | min ms | max ms | % |", "|---|---|---|---|---|---|---|"]
@@ -34,63 +69,102 @@ def main(tag):
         out.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
                    f"{float(r['AverageNs']) / 1e6:.4f} | {float(r['MinNs']) / 1e6:.4f} | {float(r['MaxNs']) / 1e6:.4f} | "
                    f"{float(r['Percentage']):.2f} |")
-    pmc = defaultdict(lambda: defaultdict(list))
-    meta = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_tcc"):
-        f = src / sub / "run_counter_collection.csv"
-        if not f.exists():
-            continue
-        for r in csv.DictReader(open(f)):
-            if "akr::" not in r["Kernel_Name"]:
-                continue
-            k = short(r["Kernel_Name"])
-            pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"], r["Scratch_Size"], r["Grid_Size"])
-    out += ["", "## Per-launch counters (separate `--pmc` passes, `--kernel-trace` only beside them)", "",
-            "| kernel | VGPR | SGPR | LDS B | scratch | grid | FETCH_SIZE KiB | HBM read MB (2x FETCH) | "
-            "WRITE_SIZE MB | TCC_MISS x 128 B MB | L2 hit % |", "|---|---|---|---|---|---|---|---|---|---|---|"]
-    traffic = {}
-    for k, c in sorted(pmc.items()):
-        fs = sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"]) if c["FETCH_SIZE"] else float("nan")
-        ws = sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"]) if c["WRITE_SIZE"] else 0.0
-        traffic[k] = {"hbm_bytes_per_launch": 2 * fs * 1024 + ws * 1024, "read_bytes": 2 * fs * 1024,
-                      "write_bytes": ws * 1024, "launches_sampled": len(c["FETCH_SIZE"])}
-        hit = sum(c["TCC_HIT_sum"]) / max(1, len(c["TCC_HIT_sum"]))
-        miss = sum(c["TCC_MISS_sum"]) / max(1, len(c["TCC_MISS_sum"]))
-        m = meta[k]
-        out.append(f"| {k} | {m[0]} | {m[1]} | {m[2]} | {m[3]} | {m[4]} | {fs:.0f} | {2 * fs * 1024 / 1e6:.1f} | "
-                   f"{ws * 1024 / 1e6:.1f} | {miss * 128 / 1e6:.1f} | {100 * hit / max(1.0, hit + miss):.1f} |")
-    workload = None
-    for log in ("pmc_fetch.log",):
-        p = src / log
-        if p.exists():
-            lines = [l for l in p.read_text().splitlines() if l.startswith("{")]
-            if lines:
-                line = json.loads(lines[-1])
-                workload = line["config"]
-                # a persistent path launch renders every spp of its call: bytes per sample pass
-                # (bench.py launches warmup W, timed K and an untimed breakdown of min(K, 4) spp)
-                K, Wm = line["steps"], line["warmup"]
-                spp_total = (Wm if Wm > 0 else 0) + K + min(K, 4)
-                for k, t in traffic.items():
-                    # not the counting builds (k_path<true, ...>; the second argument is the LDS-table flag)
-                    if k.startswith("k_path") and "<true" not in k and t["launches_sampled"]:
-                        t["hbm_bytes_per_spp"] = t["hbm_bytes_per_launch"] * t["launches_sampled"] / spp_total
-    (dst / f"{tag}_traffic.json").write_text(json.dumps(
-        {"tag": tag, "workload": workload, "source": f"profiles/{tag}_pmc_fetch.csv + {tag}_pmc_write.csv",
-         "kernels": traffic}, indent=1) + "\n")
-    for log in ("kt.log",):
-        p = src / log
-        if p.exists():
-            lines = [l for l in p.read_text().splitlines() if l.startswith("{")]
-            if lines:
-                out += ["", "## bench.py line of the kernel-trace pass", "", "```", lines[-1], "```"]
-    (dst / f"{tag}_summary.md").write_text("\n".join(out) + "\n")
-    shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
-    for sub in ("pmc_fetch", "pmc_write", "pmc_tcc"):
+    kt_line = bench_line(src / "kt.log")
+    if kt_line:
+        out += ["", "## bench.py line of the kernel-trace pass", "", "```", json.dumps(kt_line), "```"]
+
+    passes, meta = {}, {}
+    for sub in PASSES:
         f = src / sub / "run_counter_collection.csv"
         if f.exists():
-            shutil.copy(f, dst / f"{tag}_{sub}.csv")
+            passes[sub], m = read_pass(f)
+            meta.update(m)
+    line = bench_line(src / "fetch.log") or bench_line(src / "pmc_fetch.log") or kt_line
+    workload = line["config"] if line else None
+    timed_spp = line["steps"] * line["config"].get("spp_per_step", 1) if line else None
+
+    # per kernel: the timed dispatch of a path kernel (longest in each pass), else the mean over dispatches
+    kernels = {}
+    for k in sorted({k for p in passes.values() for k in p}):
+        rec = {"counters": {}}
+        for sub, p in passes.items():
+            ds = p.get(k)
+            if not ds:
+                continue
+            if is_path_kernel(k):
+                d = max(ds.values(), key=lambda x: x["dur_ns"])
+                rec.setdefault("timed_dur_ms", []).append(round(d["dur_ns"] / 1e6, 3))
+                for c, v in d.items():
+                    if c != "dur_ns":
+                        rec["counters"][c] = v
+            else:
+                for c in {c for d in ds.values() for c in d if c != "dur_ns"}:
+                    vals = [d[c] for d in ds.values() if c in d]
+                    rec["counters"][c] = sum(vals) / len(vals)
+                rec["launches_sampled"] = max(rec.get("launches_sampled", 0), len(ds))
+        if k in meta:
+            rec["grid_threads"] = int(meta[k][5])
+        c = rec["counters"]
+        if "FETCH_SIZE" in c:
+            rec["read_bytes"] = 2 * c["FETCH_SIZE"] * 1024
+            rec["write_bytes"] = c.get("WRITE_SIZE", 0.0) * 1024
+            rec["hbm_bytes_per_launch"] = rec["read_bytes"] + rec["write_bytes"]
+            if is_path_kernel(k) and timed_spp:
+                rec["timed_spp"] = timed_spp
+                rec["hbm_bytes_per_spp"] = rec["hbm_bytes_per_launch"] / timed_spp
+        if "TCC_REQ_sum" in c:
+            rec["l2_req_bytes_per_launch"] = c["TCC_REQ_sum"] * 128
+            if is_path_kernel(k) and timed_spp:
+                rec["l2_req_bytes_per_spp"] = rec["l2_req_bytes_per_launch"] / timed_spp
+        kernels[k] = rec
+
+    out += ["", "## Per-launch counters (the timed launch for the persistent path kernel; mean per launch otherwise)", "",
+            "| kernel | VGPR | AGPR | SGPR | LDS B | scratch | grid | HBM read MB (2x FETCH) | WRITE_SIZE MB | "
+            "TCC_MISS x 128 B MB | L2 hit % | TCC_REQ x 128 B GB |", "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    for k, rec in kernels.items():
+        c = rec["counters"]
+        m = meta.get(k, ("",) * 6)
+        hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+        out.append(f"| {k} | {m[0]} | {m[1]} | {m[2]} | {m[3]} | {m[4]} | {m[5]} | "
+                   f"{rec.get('read_bytes', float('nan')) / 1e6:.1f} | {rec.get('write_bytes', float('nan')) / 1e6:.1f} | "
+                   f"{miss * 128 / 1e6:.1f} | {100 * hit / max(1.0, hit + miss):.1f} | "
+                   f"{c.get('TCC_REQ_sum', float('nan')) * 128 / 1e9:.2f} |")
+    path = [k for k in kernels if is_path_kernel(k)]
+    for k in path:
+        rec, c = kernels[k], kernels[k]["counters"]
+        out += ["", f"## The timed `{k}` launch ({rec.get('timed_spp')} spp)", ""]
+        out.append(f"- launch duration in each pass (ms): {rec.get('timed_dur_ms')}")
+        if "hbm_bytes_per_spp" in rec:
+            out.append(f"- HBM (L2 -> fabric) bytes per sample pass: {rec['hbm_bytes_per_spp'] / 1e9:.3f} GB "
+                       f"(read {rec['read_bytes'] / rec['timed_spp'] / 1e9:.3f}, write {rec['write_bytes'] / rec['timed_spp'] / 1e9:.3f})")
+        if "l2_req_bytes_per_spp" in rec:
+            out.append(f"- L2 requests x 128 B per sample pass: {rec['l2_req_bytes_per_spp'] / 1e9:.3f} GB")
+        if "SQ_WAVE_CYCLES" in c:
+            wc = c["SQ_WAVE_CYCLES"]
+            out.append(f"- wave time: parked in s_waitcnt (SQ_WAIT_ANY) {100 * c['SQ_WAIT_ANY'] / wc:.1f} %, "
+                       f"issue-stalled (SQ_WAIT_INST_ANY) {100 * c['SQ_WAIT_INST_ANY'] / wc:.1f} %, issuing (SQ_ACTIVE_INST_ANY) "
+                       f"{100 * c['SQ_ACTIVE_INST_ANY'] / wc:.1f} %; VALU active {100 * c['SQ_ACTIVE_INST_VALU'] / wc:.1f} %")
+        if "VmemLatency" in c:
+            out.append(f"- VmemLatency (issue to return of a VMEM instruction, mean): {c['VmemLatency']:.0f} cycles")
+        if "TCP_TCC_READ_REQ_sum" in c and c["TCP_TCC_READ_REQ_sum"]:
+            out.append(f"- TCP -> TCC read latency: {c['TCP_TCC_READ_REQ_LATENCY_sum'] / c['TCP_TCC_READ_REQ_sum']:.0f} cycles "
+                       f"mean over {c['TCP_TCC_READ_REQ_sum']:.3g} requests")
+        if "TCC_EA0_RDREQ_sum" in c and c["TCC_EA0_RDREQ_sum"]:
+            out.append(f"- L2 -> fabric read requests: {c['TCC_EA0_RDREQ_sum']:.3g}, mean in flight x time / count = "
+                       f"{c['TCC_EA0_RDREQ_LEVEL_sum'] / c['TCC_EA0_RDREQ_sum']:.0f} cycles per request")
+    (dst / f"{tag}_traffic.json").write_text(json.dumps(
+        {"tag": tag, "command": f"python3 bench.py {args}", "workload": workload,
+         "source": f"profiles/{tag}_*.csv (tools/profile_driver.sh)", "kernels": kernels}, indent=1) + "\n")
+    (dst / f"{tag}_summary.md").write_text("\n".join(out) + "\n")
+    shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
+    for sub in PASSES:
+        f = src / sub / "run_counter_collection.csv"
+        if f.exists():
+            # only the akr kernels' rows (the runtime's copy kernels make the files large)
+            rows = [r for r in csv.reader(open(f))]
+            keep = [rows[0]] + [r for r in rows[1:] if any("akr::" in x for x in r)]
+            with open(dst / f"{tag}_{sub}.csv", "w", newline="") as fo:
+                csv.writer(fo).writerows(keep)
     print((dst / f"{tag}_summary.md").read_text())
 
 
