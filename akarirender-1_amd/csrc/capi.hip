@@ -291,6 +291,9 @@ struct akr_hip_ctx {
     int64_t path_order_share_pixels = 1200000;
     int path_order_share_min_spp = 16;
     int path_order_shift = 2;
+    // option "path_order_classes": at most this many cost classes (1..32), the costliest holding every
+    // pixel above; fewer classes keep more of the tile order inside a shard
+    int path_order_classes = 32;
     // option "path_order_cap": a pilot ray stops after this many steps (0: none); its cost class is
     // then the cap's.  The pilot is a small latency-bound launch whose length is set by its slowest
     // ray, while the order only needs coarse classes (soup against background).
@@ -740,7 +743,8 @@ struct akr_hip_ctx {
         t.step_cap = (uint32_t)path_order_cap;
         // the steps-only build: no hits, no tallies (the counting build spilled and ran ~20 % longer)
         launch_trace(TRACE_PILOT, false, true, true, t, grid_for(TRACE_CLOSEST, n_rays), ms);
-        launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, sub, d_okey[0].p, d_oidx[0].p, ms);
+        launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, (uint32_t)(path_order_classes - 1), sub,
+                          d_okey[0].p, d_oidx[0].p, ms);
         sort_pixel_order(d_otmp.p, tb, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
         HIPCHK(hipGetLastError());
     }
@@ -1329,6 +1333,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_sub") {
             if (value < 0 || value > 5) throw std::runtime_error("path_order_sub must be in [0, 5]");
             ctx->path_order_sub = (int)value;
+        } else if (k == "path_order_classes") {
+            if (value < 1 || value > 32) throw std::runtime_error("path_order_classes must be in [1, 32]");
+            ctx->path_order_classes = (int)value;
         } else if (k == "path_order_shift") {
             if (value < 0 || value > 31) throw std::runtime_error("path_order_shift must be in [0, 31]");
             ctx->path_order_shift = (int)value;

@@ -36,8 +36,8 @@ void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream
 constexpr uint32_t kOrderClassBits = 5, kOrderClassMask = (1u << kOrderClassBits) - 1u;
 void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, uint32_t sub, float4 *rays,
                        hipStream_t st);
-void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t sub, uint32_t *key, uint32_t *idx,
-                       hipStream_t st);
+void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t cmax, uint32_t sub, uint32_t *key,
+                       uint32_t *idx, hipStream_t st);
 size_t pixel_order_tmp_bytes(uint32_t n);
 void sort_pixel_order(void *tmp, size_t tmp_bytes, const uint32_t *key_in, uint32_t *key_out, const uint32_t *idx_in,
                       uint32_t *idx_out, uint32_t n, hipStream_t st);

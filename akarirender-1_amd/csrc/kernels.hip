@@ -2324,16 +2324,17 @@ __global__ __launch_bounds__(kBlock) void k_pilot_rays(CameraDev cam, const uint
     rays[2 * (size_t)i + 1] = r1;
 }
 
-// Sort key of slot i: its XCD shard above its cost class (steps >> shift, capped, descending), so a
-// stable sort orders each shard by decreasing cost and keeps tile order within a class.
-__global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t sub,
-                                                       uint32_t *key, uint32_t *idx) {
+// Sort key of slot i: its XCD shard above its cost class (steps >> shift, capped at cmax <=
+// kOrderClassMask, descending), so a stable sort orders each shard by decreasing cost and keeps tile
+// order within a class (few classes keep more of the tile order: a smaller cache footprint).
+__global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t cmax,
+                                                       uint32_t sub, uint32_t *key, uint32_t *idx) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     uint32_t sh = 0;
     for (uint32_t k = 1; k < kWorkShards; k++) sh += i >= shard_begin(n, k) ? 1u : 0u;
     const uint32_t s = steps[i >> sub];  // 0xFFFFFFFF: traced by the exact BVH2 walk (rare): costliest class
-    const uint32_t cls = s == 0xFFFFFFFFu ? kOrderClassMask : min(s >> shift, kOrderClassMask);
+    const uint32_t cls = s == 0xFFFFFFFFu ? cmax : min(s >> shift, cmax);
     key[i] = (sh << kOrderClassBits) | (kOrderClassMask - cls);
     idx[i] = i;
 }
@@ -2482,10 +2483,11 @@ void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, 
     if (n == 0) return;
     hipLaunchKernelGGL(k_pilot_rays, dim3(blocks_for(n)), dim3(kBlock), 0, st, cam, pixel, n, sub, rays);
 }
-void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t sub, uint32_t *key, uint32_t *idx,
-                       hipStream_t st) {
+void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t cmax, uint32_t sub, uint32_t *key,
+                       uint32_t *idx, hipStream_t st) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift, sub, key, idx);
+    hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift,
+                       cmax < kOrderClassMask ? cmax : kOrderClassMask, sub, key, idx);
 }
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st) {
     if (n == 0) return;
