@@ -252,12 +252,17 @@ struct akr_hip_ctx {
     DBuf<uint32_t> d_work;  // dynamic-fetch counters of a standalone trace launch (kTraceWords)
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
-    uint32_t path_grid[2][2] = {{0, 0}, {0, 0}};  // resident workgroups of the persistent path kernels [defer][tab]
+    uint32_t path_grid[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // resident workgroups of the persistent path kernels [kind][tab]
     // option "path_defer": 1 = k_path_defer (max_depth <= 8), 0 = k_path, 2 (default) = k_path_defer for
     // renders of at most path_defer_pixels pixels (measured on C3, DESIGN.md §3.9: 13 % faster on an
     // 8-way share and 4 % on a 4-way one, 1 % slower on a 2-way share and 5 % on the whole frame,
     // whose lanes seldom have spare capacity)
     int path_defer = 2;
+    // option "path_spec": k_path_spec (lanes left idle by the drained pixel queue run
+    // the next sample of a busy pixel from a guessed sampler state; committed in order, bit-exact):
+    // 1 = always, 0 = never, 2 = for renders of at most path_spec_pixels pixels
+    int path_spec = 0;
+    int64_t path_spec_pixels = 600000;
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
@@ -576,9 +581,9 @@ struct akr_hip_ctx {
             trace_grid[m] = (uint32_t)(n_cu * trace_blocks_per_cu(m));
             mx = std::max(mx, trace_grid[m]);
         }
-        for (int d = 0; d < 2; d++)
+        for (int d = 0; d < 3; d++)
             for (int t = 0; t < 2; t++) {
-                path_grid[d][t] = (uint32_t)(n_cu * path_blocks_per_cu(d != 0, t != 0));
+                path_grid[d][t] = (uint32_t)(n_cu * path_blocks_per_cu(d, t != 0));
                 mx = std::max(mx, path_grid[d][t]);
             }
         ovf_threads = mx * kTraceBlock;
@@ -987,13 +992,16 @@ struct akr_hip_ctx {
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels &&
                                                         (int64_t)n_tris() >= path_defer_min_tris));
+                // speculative samples on the lanes a drained queue leaves idle
+                const bool spec = path_spec == 1 || (path_spec == 2 && (int64_t)N <= path_spec_pixels);
+                const int kind = spec ? PATH_SPEC : (defer ? PATH_DEFER : PATH_PLAIN);
                 // the shading's material / light / CDF tables in LDS when they fit
                 const bool tab = path_tab && path_tab_fits(n_mats, n_lights);
-                const uint64_t resident = (uint64_t)path_grid[defer][tab] * (uint64_t)path_grid_pct / 100;
+                const uint64_t resident = (uint64_t)path_grid[kind][tab] * (uint64_t)path_grid_pct / 100;
                 const uint32_t grid = (uint32_t)std::max<uint64_t>(
                     1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
                 pa.min_wait = (uint32_t)(path_min_wait > 0 ? path_min_wait : 40);
-                if (defer) {
+                if (kind == PATH_DEFER) {
                     d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
                     pa.contrib = d_contrib.p;
                     pa.mix = path_mix ? 1u : 0u;
@@ -1007,17 +1015,17 @@ struct akr_hip_ctx {
                 const int order_min_spp = (int64_t)N <= path_order_share_pixels
                                               ? std::min(path_order_share_min_spp, path_order_min_spp)
                                               : path_order_min_spp;
-                if (path_order != 0 && (!defer || path_order == 2) && p.spp >= order_min_spp && N >= 2) {
+                if (path_order != 0 && (kind == PATH_PLAIN || path_order == 2) && p.spp >= order_min_spp && N >= 2) {
                     timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
                     pa.order = d_oidx[1].p;
                     const bool pair = path_order_pair == 3 ||
-                                      (defer && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000)));
+                                      (kind != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000)));
                     pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
                     pa.prio = (uint32_t)path_prio;
                 }
-                timed("path", ms, [&] { launch_path(count, defer, tab, pa, grid, ms); });
+                timed("path", ms, [&] { launch_path(count, kind, tab, pa, grid, ms); });
                 HIPCHK(hipGetLastError());
-                last_form = defer ? AKR_FORM_PATH_DEFER : AKR_FORM_PATH;
+                last_form = kind == PATH_SPEC ? AKR_FORM_PATH_SPEC : (kind == PATH_DEFER ? AKR_FORM_PATH_DEFER : AKR_FORM_PATH);
                 last_ordered = pa.order ? 1 : 0;
             }
             last_passes = 1;
@@ -1350,6 +1358,12 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_mix = value != 0;
         } else if (k == "path_tab") {
             ctx->path_tab = value != 0;
+        } else if (k == "path_spec") {
+            if (value < 0 || value > 2) throw std::runtime_error("path_spec must be 0, 1 or 2");
+            ctx->path_spec = (int)value;
+        } else if (k == "path_spec_pixels") {
+            if (value < 0) throw std::runtime_error("path_spec_pixels must be >= 0");
+            ctx->path_spec_pixels = value;
         } else if (k == "path_grid_pct") {
             if (value < 1 || value > 100) throw std::runtime_error("path_grid_pct must be in [1, 100]");
             ctx->path_grid_pct = (int)value;

@@ -20,8 +20,10 @@ void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st);
 void launch_la_accept(const LookArgs &a, uint32_t max_active, hipStream_t st);
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t st);
-void launch_path(bool count, bool defer, bool tab, const PathArgs &a, uint32_t grid, hipStream_t st);
-int path_blocks_per_cu(bool defer, bool tab);
+// persistent path kernel forms
+enum : int { PATH_PLAIN = 0, PATH_DEFER = 1, PATH_SPEC = 2 };
+void launch_path(bool count, int kind, bool tab, const PathArgs &a, uint32_t grid, hipStream_t st);
+int path_blocks_per_cu(int kind, bool tab);
 bool path_tab_fits(int32_t n_mats, int32_t n_lights);
 void launch_check_weights(const float4 *film, uint32_t n, float expect, uint32_t *bad, hipStream_t st);
 void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t *order, uint32_t n, int32_t width,

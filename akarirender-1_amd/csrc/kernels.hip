@@ -2252,6 +2252,381 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 
 #undef DEFER_SPLAT
 
+// ------------------------------------------------------------- persistent path, speculative samples
+// k_path_spec: k_path whose lanes, once the pixel queue is drained, run the NEXT
+// sample of a busy pixel of their wave speculatively.  A pixel's samples are sequential only
+// through its sampler state (cpu/integrator.cpp:124-134): sample s + 1 starts where sample s
+// stopped drawing, 4 + 6 k draws later for k scattering events (pathtracer.h:96-164).  The helper
+// starts sample s + 1 from the guessed state lcg_advance(start(s), g) with g = 4 + 6 max_depth (a
+// full-length path: on the C3 soup the costliest pixels' samples are full length 91-100 % of the
+// time, tools/sample_lengths.py), while the pixel's owner runs sample s.  Samples are committed in
+// order by the owner: the head (the one that started from the committed state C) is added to the
+// film and C becomes its end state E; the other sample is kept iff it started from exactly E (it is
+// then the sequential sample s + 1, bit for bit), otherwise it is dropped and rerun.  So the film
+// sums and the final sampler state are the sequential loop's.  At most two samples of a pixel are
+// in flight (its head and one successor), on the owner's lane and its helper's.  Every hand-off is a
+// lane shuffle inside one wave.
+enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
+enum : uint32_t { CMD_NONE = 0, CMD_CONSUMED = 1, CMD_ABORT = 2, CMD_RELEASE = 3 };
+
+struct SpecState {
+    uint32_t w = 0;
+    // ROLE: free / owner / helper; PART: the partner lane (owner: its helper, helper: its owner) when
+    // HASP; SRUN: the lane runs a sample; SEND: its sample ended, (Lr, seed) wait to be committed;
+    // HEADH (owner): the helper's sample is the head; NIF (owner): the pixel's samples in flight
+    static constexpr uint32_t ROLE = 0, PART = 2, HASP = 8, SRUN = 9, SEND = 10, HEADH = 11, NIF = 12, ANY = 14, PEND = 15;
+    __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
+    __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
+        const uint32_t m = ((1u << bits) - 1u) << off;
+        w = (w & ~m) | ((v << off) & m);
+    }
+    __device__ __forceinline__ uint32_t role() const { return get(ROLE, 2); }
+    __device__ __forceinline__ uint32_t part() const { return get(PART, 6); }
+    __device__ __forceinline__ bool hasp() const { return get(HASP, 1) != 0; }
+    __device__ __forceinline__ bool srun() const { return get(SRUN, 1) != 0; }
+    __device__ __forceinline__ bool send() const { return get(SEND, 1) != 0; }
+    __device__ __forceinline__ bool headh() const { return get(HEADH, 1) != 0; }
+    __device__ __forceinline__ uint32_t nif() const { return get(NIF, 2); }
+    __device__ __forceinline__ bool any() const { return get(ANY, 1) != 0; }
+    __device__ __forceinline__ bool pend() const { return get(PEND, 1) != 0; }
+};
+
+template <bool COUNT, bool TAB>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_spec(PathArgs pa) {
+    const TraceArgs &a = pa.t;
+    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
+    __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
+    lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
+    glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gtid = blockIdx.x * kTraceBlock + tid;
+    const uint32_t lane = __lane_id();
+    const uint32_t n = pa.n_pix;
+    const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
+    const uint32_t guess = 4u + 6u * (uint32_t)pa.max_depth;  // draws of a full-length sample
+    const bool ff = a.any_far_first != 0;
+    const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
+    PathCount c;
+    PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
+    f.s_lo = shard_begin(n, f.shard);
+    f.s_hi = shard_begin(n, f.shard + 1);
+
+    // owner: its pixel, the samples not yet started, the film sums; every lane: the sample it runs
+    uint32_t pix = 0, left = 0, seed = 0, sstart = 0;
+    int depth = 0;
+    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f};
+    float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
+    SpecState s;
+    s.set(SpecState::PART, 6, lane);
+    bool done = false, fin = false, busy = false;
+    uint32_t idle_rounds = 0;
+    uint32_t pc_closest = 0, pc_shadow = 0, sc_closest = 0, sc_shadow = 0;  // counting build: pixel / sample rays
+    PathRay r{};
+    r.best = kInf;
+    r.bgid = kNoHit;
+    r.cur = r.leaf = AKR_CHILD_EMPTY;
+    unsigned long long p_outer = 0, p_procs = 0, p_tp = 0, p_tt = 0, p_tl = 0, p_lanes = 0, p_t0 = 0, p_t = 0, p_tsh = 0;
+    if (COUNT) p_t0 = wall_clock64();
+
+    while (true) {
+        if (!__any(s.role() != ROLE_FREE || !done || busy || fin)) break;
+        const uint32_t nfin = (uint32_t)__popcll(__ballot(fin));
+        const uint32_t nbusy = (uint32_t)__popcll(__ballot(busy));
+        if (COUNT) {
+            p_outer++;
+            p_t = wall_clock64();
+        }
+        if (nfin > 0 ? 64u * nfin >= pa.min_wait * (nfin + nbusy) : nbusy == 0) {
+            if (COUNT) {
+                p_procs++;
+                p_lanes += nfin;
+            }
+            path_park(s_park, tid, r);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            asm volatile("" ::: "memory");
+            bool fresh = false, next_any = false, abort_self = false, start = false;
+            float4 ra = {}, rb = {};
+            unsigned long long p_ts = 0;
+            if (COUNT) p_ts = wall_clock64();
+            // 1. the finished ray (k_path's processing); a sample that ended waits for its commit
+            if (fin) {
+                fin = false;
+                bool sample_end = false;
+                const uint32_t hgid = r.bgid;
+                if (s.any()) {  // shadow ray: NEE contribution when unoccluded (pathtracer.h:84-88)
+                    if (hgid == kNoHit) {
+                        Lr.x += scol.x;
+                        Lr.y += scol.y;
+                        Lr.z += scol.z;
+                    }
+                    if (s.pend()) {
+                        ra = pe0;
+                        rb = pe1;
+                        fresh = true;
+                        s.set(SpecState::PEND, 1, 0);
+                    } else {
+                        sample_end = true;
+                    }
+                } else if (hgid == kNoHit) {  // on_miss: the sample ends
+                    sample_end = true;
+                } else {
+                    const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
+                    Bounce bo;
+                    shade_hit_tab(pa.sc, tab, hgid, r.bu, r.bv, wo, beta, seed, depth, pa.max_depth, depth == nb - 1, bo);
+                    if (bo.emit) {
+                        Lr.x += bo.e.x;
+                        Lr.y += bo.e.y;
+                        Lr.z += bo.e.z;
+                    }
+                    if (bo.ext) {
+                        beta = bo.nb;
+                        depth++;
+                    }
+                    if (bo.sh) {  // the shadow ray first, the extension ray waits behind it
+                        ra = bo.s0;
+                        rb = bo.s1;
+                        scol = bo.col;
+                        next_any = true;
+                        fresh = true;
+                        s.set(SpecState::PEND, 1, bo.ext ? 1u : 0u);
+                        pe0 = bo.e0;
+                        pe1 = bo.e1;
+                    } else if (bo.ext) {
+                        ra = bo.e0;
+                        rb = bo.e1;
+                        fresh = true;
+                    } else {
+                        sample_end = true;
+                    }
+                }
+                if (sample_end) {
+                    s.set(SpecState::SRUN, 1, 0);
+                    s.set(SpecState::SEND, 1, 1);
+                }
+            }
+            if (COUNT) p_tsh += wall_clock64() - p_ts;
+            // 2. owners commit their samples in order; every lane reads its partner's sample
+            {
+                const int part = (int)s.part();
+                const uint32_t p_send = (uint32_t)__shfl((int)s.get(SpecState::SEND, 1), part);
+                const uint32_t p_start = (uint32_t)__shfl((int)sstart, part);
+                const uint32_t p_end = (uint32_t)__shfl((int)seed, part);
+                V3 p_L;
+                p_L.x = __shfl(Lr.x, part);
+                p_L.y = __shfl(Lr.y, part);
+                p_L.z = __shfl(Lr.z, part);
+                uint32_t p_cc = 0, p_cs = 0;
+                if (COUNT) {
+                    p_cc = (uint32_t)__shfl((int)sc_closest, part);
+                    p_cs = (uint32_t)__shfl((int)sc_shadow, part);
+                }
+                uint32_t cmd = CMD_NONE;
+                if (s.role() == ROLE_OWNER) {
+                    uint32_t nif = s.nif();
+                    for (int it = 0; it < 2 && nif > 0; it++) {
+                        const bool headh = s.headh();
+                        if (!(headh ? p_send != 0 : s.send())) break;
+                        const V3 L = headh ? p_L : Lr;
+                        const uint32_t E = headh ? p_end : seed;
+                        splat_one(film, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);  // Tile::add_sample
+                        if (COUNT) {
+                            pc_closest += headh ? p_cc : sc_closest;
+                            pc_shadow += headh ? p_cs : sc_shadow;
+                        }
+                        if (headh) cmd = CMD_CONSUMED;
+                        else s.set(SpecState::SEND, 1, 0);
+                        nif--;
+                        if (nif == 1) {  // the other sample is the next one iff it started from E
+                            const uint32_t o_start = headh ? sstart : p_start;
+                            if (o_start == E) {
+                                s.set(SpecState::HEADH, 1, headh ? 0u : 1u);
+                                continue;
+                            }
+                            if (headh) abort_self = true;  // the owner's own successor
+                            else cmd = CMD_ABORT;
+                            left++;
+                            nif = 0;
+                        }
+                        seed = E;  // nothing in flight: the owner's lane holds the committed state
+                    }
+                    s.set(SpecState::NIF, 2, nif);
+                    if (nif == 0 && left == 0 && !s.srun() && !s.send()) {  // the pixel is done
+                        pa.film[pix] = film;
+                        if (pa.probe)
+                            pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
+                                                       COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
+                        if (s.hasp()) cmd = CMD_RELEASE;
+                        s.set(SpecState::ROLE, 2, ROLE_FREE);
+                        s.set(SpecState::HASP, 1, 0);
+                        s.set(SpecState::PART, 6, lane);
+                    }
+                }
+                // 3. helpers apply their owner's decision
+                const uint32_t hcmd = (uint32_t)__shfl((int)cmd, part);
+                if (s.role() == ROLE_HELPER) {
+                    if (hcmd == CMD_CONSUMED) {
+                        s.set(SpecState::SEND, 1, 0);
+                    } else if (hcmd == CMD_ABORT) {
+                        abort_self = true;
+                    } else if (hcmd == CMD_RELEASE) {  // the pixel is done: nothing of it is in flight
+                        s.set(SpecState::ROLE, 2, ROLE_FREE);
+                        s.set(SpecState::HASP, 1, 0);
+                        s.set(SpecState::PART, 6, lane);
+                        s.set(SpecState::SRUN, 1, 0);
+                        s.set(SpecState::SEND, 1, 0);
+                    }
+                }
+                if (abort_self) {  // a dropped speculation: its ray (in flight or fresh) goes with it
+                    s.set(SpecState::SRUN, 1, 0);
+                    s.set(SpecState::SEND, 1, 0);
+                    s.set(SpecState::PEND, 1, 0);
+                    fresh = false;
+                    busy = false;
+                }
+            }
+            // 4. free lanes fetch the next pixel while the queue lasts
+            {
+                bool need = s.role() == ROLE_FREE && !done;
+                const bool asked = need;
+                fetch_pixels(f, n, pa.work, pa.order ? pa.order_mode : FETCH_LINEAR, pa.order, pa.prio, need, done, pix);
+                if (asked && !need) {
+                    const uint32_t px = pa.pixel[pix];
+                    left = pa.spp;
+                    seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                    film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    s.set(SpecState::ROLE, 2, ROLE_OWNER);
+                    s.set(SpecState::NIF, 2, 0);
+                    s.set(SpecState::HEADH, 1, 0);
+                    if (COUNT) pc_closest = pc_shadow = 0;
+                }
+            }
+            // 5. lanes with nothing left to fetch become helpers of owners with samples to start
+            {
+                const bool avail = s.role() == ROLE_FREE && done;
+                const bool want = s.role() == ROLE_OWNER && !s.hasp() && left > 0;
+                const unsigned long long fm = __ballot(avail), om = __ballot(want);
+                if (fm && om) {
+                    const uint32_t k = min((uint32_t)__popcll(fm), (uint32_t)__popcll(om));
+                    if (avail) {
+                        const uint32_t fr = lane_prefix(fm);
+                        if (fr < k) {
+                            s.set(SpecState::ROLE, 2, ROLE_HELPER);
+                            s.set(SpecState::PART, 6, (uint32_t)nth_set_bit(om, fr));
+                            s.set(SpecState::HASP, 1, 1);
+                        }
+                    }
+                    if (want) {
+                        const uint32_t orank = lane_prefix(om);
+                        if (orank < k) {
+                            s.set(SpecState::PART, 6, (uint32_t)nth_set_bit(fm, orank));
+                            s.set(SpecState::HASP, 1, 1);
+                        }
+                    }
+                }
+            }
+            // 6. the owner starts samples: its head from C, or the successor of the head from the
+            // guessed state, on its own lane and on its helper's
+            {
+                const int part = (int)s.part();
+                const uint32_t p_idle = (uint32_t)__shfl((int)((s.srun() || s.send()) ? 0u : 1u), part);
+                const uint32_t p_start = (uint32_t)__shfl((int)sstart, part);
+                uint32_t hstart = 0, hgo = 0;
+                if (s.role() == ROLE_OWNER) {
+                    uint32_t nif = s.nif();
+                    if (!s.srun() && !s.send() && left > 0) {
+                        if (nif == 0) {  // the head, from the committed state
+                            sstart = seed;
+                            start = true;
+                            left--;
+                            nif = 1;
+                            s.set(SpecState::HEADH, 1, 0);
+                        } else if (nif == 1 && s.headh()) {  // the helper runs the head: its successor here
+                            seed = lcg_advance(p_start, guess);
+                            sstart = seed;
+                            start = true;
+                            left--;
+                            nif = 2;
+                        }
+                    }
+                    if (s.hasp() && p_idle && left > 0 && nif == 1 && !s.headh()) {  // successor on the helper
+                        hstart = lcg_advance(sstart, guess);
+                        hgo = 1;
+                        left--;
+                        nif = 2;
+                    }
+                    s.set(SpecState::NIF, 2, nif);
+                }
+                const uint32_t go = (uint32_t)__shfl((int)hgo, part);
+                const uint32_t gstate = (uint32_t)__shfl((int)hstart, part);
+                const uint32_t opix = (uint32_t)__shfl((int)pix, part);
+                if (s.role() == ROLE_HELPER && go) {
+                    seed = gstate;
+                    sstart = gstate;
+                    start = true;
+                }
+                if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
+                    const uint32_t px = pa.pixel[s.role() == ROLE_HELPER ? opix : pix];
+                    Lr = V3{0.0f, 0.0f, 0.0f};
+                    beta = V3{1.0f, 1.0f, 1.0f};
+                    depth = 0;
+                    camera_ray(pa.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, ra, rb);
+                    s.set(SpecState::SRUN, 1, 1);
+                    s.set(SpecState::PEND, 1, 0);
+                    next_any = false;
+                    fresh = true;
+                    if (COUNT) sc_closest = sc_shadow = 0;
+                }
+            }
+            asm volatile("" ::: "memory");
+            path_unpark(s_park, tid, r, ff, s.any());  // the busy lanes' traversal continues unchanged
+            if (fresh) {
+                s.set(SpecState::ANY, 1, next_any ? 1u : 0u);
+                if (COUNT) {
+                    sc_closest += next_any ? 0u : 1u;
+                    sc_shadow += next_any ? 1u : 0u;
+                }
+                busy = path_begin<COUNT>(a, next_any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
+                fin = !busy;
+            }
+        }
+        if (COUNT) {
+            const unsigned long long t = wall_clock64();
+            p_tp += t - p_t;
+            p_t = t;
+        }
+        if (!__any(busy)) {
+            // nothing in flight: the next processing phase commits or starts something; a wave that
+            // idles for many rounds has lost its state (a bug): stop and raise the fault word
+            if (++idle_rounds > 1024) {
+                if (pa.fault && __lane_id() == 0) __hip_atomic_fetch_or(pa.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            continue;
+        }
+        idle_rounds = 0;
+        // ---- B. traversal phase, C. leaf phase (k_trace's, shared with the other persistent kernels)
+        const int kd = s.any() ? 1 : 0;
+        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
+        if (COUNT) {
+            const unsigned long long t = wall_clock64();
+            p_tt += t - p_t;
+            p_t = t;
+        }
+        const bool hit_any = path_leaf<COUNT>(busy, kd, r, a.wide_leaves, c);
+        if (busy && (hit_any || r.cur == AKR_CHILD_EMPTY)) {
+            busy = false;
+            fin = true;
+            if (COUNT) c.deep[kd] += c.deep_now ? 1 : 0;
+        }
+        if (COUNT) p_tl += wall_clock64() - p_t;
+    }
+    if (COUNT) path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
+    if (pa.fault_test && pa.fault && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_or(pa.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Film::merge_tile (core/film.h:85-95) on the device: a context's packed film (one float4 per
 // slot: radiance sums, weight) added into full-frame buffers at its pixels.  `order` (optional)
 // lists the slots of one launch; a launch never holds the same pixel twice, so the adds of a pixel
@@ -2442,25 +2817,29 @@ void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
     hipLaunchKernelGGL(k_splat, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
 template <bool COUNT, bool TAB>
-static void launch_path_t(bool defer, const PathArgs &a, uint32_t grid, hipStream_t st) {
-    if (defer) hipLaunchKernelGGL((k_path_defer<COUNT, TAB>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+static void launch_path_t(int kind, const PathArgs &a, uint32_t grid, hipStream_t st) {
+    if (kind == PATH_DEFER) hipLaunchKernelGGL((k_path_defer<COUNT, TAB>), dim3(grid), dim3(kTraceBlock), 0, st, a);
+    else if (kind == PATH_SPEC) hipLaunchKernelGGL((k_path_spec<COUNT, TAB>), dim3(grid), dim3(kTraceBlock), 0, st, a);
     else hipLaunchKernelGGL((k_path<COUNT, TAB>), dim3(grid), dim3(kTraceBlock), 0, st, a);
 }
-void launch_path(bool count, bool defer, bool tab, const PathArgs &a, uint32_t grid, hipStream_t st) {
+void launch_path(bool count, int kind, bool tab, const PathArgs &a, uint32_t grid, hipStream_t st) {
     if (grid == 0) return;
     if (tab && !path_tab_fits(a.sc.n_mats, a.sc.n_lights)) tab = false;  // the LDS copy must hold every record
     if (count) {
-        if (tab) launch_path_t<true, true>(defer, a, grid, st);
-        else launch_path_t<true, false>(defer, a, grid, st);
+        if (tab) launch_path_t<true, true>(kind, a, grid, st);
+        else launch_path_t<true, false>(kind, a, grid, st);
     } else {
-        if (tab) launch_path_t<false, true>(defer, a, grid, st);
-        else launch_path_t<false, false>(defer, a, grid, st);
+        if (tab) launch_path_t<false, true>(kind, a, grid, st);
+        else launch_path_t<false, false>(kind, a, grid, st);
     }
 }
-int path_blocks_per_cu(bool defer, bool tab) {
+int path_blocks_per_cu(int kind, bool tab) {
     int nb = 0;
     hipError_t e;
-    if (defer)
+    if (kind == PATH_SPEC)
+        e = tab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_spec<false, true>, kTraceBlock, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_spec<false, false>, kTraceBlock, 0);
+    else if (kind == PATH_DEFER)
         e = tab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_defer<false, true>, kTraceBlock, 0)
                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_defer<false, false>, kTraceBlock, 0);
     else

@@ -316,13 +316,15 @@ int akr_hip_reset_stats(akr_hip_ctx *ctx);
 int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
 /* Which form ran the last path render (all give the same bits): the wavefront
  * kernels (north_star's layout: raygen -> closest -> shade -> shadow -> splat launches), lookahead
- * lanes over the wavefront, the persistent path kernel, or its deferred-NEE form; *ordered = 1 when
+ * lanes over the wavefront, the persistent path kernel, its deferred-NEE form or its speculative-sample
+ * form; *ordered = 1 when
  * the persistent kernel fetched pixels in pilot-cost order.  AKR_FORM_NONE: nothing rendered. */
 #define AKR_FORM_NONE (-1)
 #define AKR_FORM_WAVEFRONT 0
 #define AKR_FORM_LOOKAHEAD 1
 #define AKR_FORM_PATH 2
 #define AKR_FORM_PATH_DEFER 3
+#define AKR_FORM_PATH_SPEC 4
 int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered);
 int akr_hip_synchronize(akr_hip_ctx *ctx);
 /* Copies the first n records of the last render's pixel probe (see akr_pixel_probe); fails when

@@ -176,10 +176,12 @@ FORMS = [
     ("k_path_defer scrambled", dict(path=1, path_defer=1, path_order=0)),
     ("k_path_defer ordered", dict(path=1, path_defer=1, path_order=2, path_order_pair=0)),
     ("k_path_defer ordered, paired", dict(path=1, path_defer=1, path_order=2, path_order_pair=1)),
+    ("k_path_spec", dict(path=1, path_defer=0, path_spec=1, path_order=0)),
+    ("k_path_spec ordered, paired", dict(path=1, path_defer=0, path_spec=1, path_order=2, path_order_pair=1)),
     ("wavefront", dict(path=0, path_defer=2, path_order=2)),
 ]
-DEFAULTS = dict(path=2, path_defer=2, path_order=2, path_order_pair=2, path_order_min_spp=16, count_tests=0,
-                pixel_probe=0)
+DEFAULTS = dict(path=2, path_defer=2, path_spec=0, path_order=2, path_order_pair=2, path_order_min_spp=16,
+                count_tests=0, pixel_probe=0)
 
 
 def _render_forms(ctx, orc_rad, orc_w, orc_probe, tiles, spp, depth):
@@ -193,7 +195,7 @@ def _render_forms(ctx, orc_rad, orc_w, orc_probe, tiles, spp, depth):
         ctx.set_option("path_order_min_spp", 0)
         for name, opts in FORMS:
             for count in ((0, 1) if opts["path"] == 1 else (0,)):
-                for k, v in opts.items():
+                for k, v in dict(dict(path_spec=0), **opts).items():
                     ctx.set_option(k, v)
                 ctx.set_option("count_tests", count)
                 what = f"{name}{' (counting build)' if count else ''}"

@@ -96,8 +96,9 @@ def test_trace_leaf_sizes(hip_ctx_factory, leaf):
         _check_trace(ctx, orc, cs, random_rays(1 << 14, 4, -1.1, 1.1), False)
         _check_trace(ctx, orc, cs, random_rays(1 << 14, 5, -1.1, 1.1), True)
         ctx.set_option("path", 1)
-        for defer in (0, 1):
-            ctx.set_option("path_defer", defer)
+        for defer in (0, 1, 2):   # k_path, k_path_defer, k_path_spec
+            ctx.set_option("path_defer", 1 if defer == 1 else 0)
+            ctx.set_option("path_spec", 1 if defer == 2 else 0)
             _check_render(ctx, orc, 2, 5, [(0, 0, 96, 54), (40, 20, 75, 50)], 96, 54, probe=True)
 
 
@@ -616,11 +617,14 @@ def _tab_fits(cs):
 
 @pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
                                                       (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
-                                                      (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2)])
+                                                      (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2),
+                                                      (1, 2, 0, 1, 0), (1, 2, 0, 0, 2), (1, 2, 0, 1, 2)])
 def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab, order):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
     §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
-    scrambled or tile-order pixel fetch) and the wavefront kernels give the oracle's image bit for
+    scrambled or tile-order pixel fetch; defer = 1), its speculative-sample form (k_path_spec, §3.11:
+    idle lanes run a busy pixel's next sample from a guessed sampler state, committed in order only
+    when the guess was the true state; defer = 2) and the wavefront kernels give the oracle's image bit for
     bit: ragged / clipped / empty tiles, depths 0-9 (above 8 the deferred form falls back to
     k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
     deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes); with the
@@ -628,7 +632,8 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
     cost-ordered pixel fetch (order, §3.10) forced on at every spp, or off."""
     def opts(ctx):
         ctx.set_option("path", path)
-        ctx.set_option("path_defer", defer)
+        ctx.set_option("path_defer", 1 if defer == 1 else 0)
+        ctx.set_option("path_spec", 1 if defer == 2 else 0)
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
         ctx.set_option("path_order", order)
