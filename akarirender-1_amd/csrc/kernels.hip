@@ -2502,25 +2502,34 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     if (COUNT) pc_closest = pc_shadow = 0;
                 }
             }
-            // 5. lanes with nothing left to fetch become helpers of owners with samples to start
+            // 5. lanes with nothing left to fetch become helpers of owners with samples to start; the
+            // owners with at least half the wave's most samples left are served first (the longest
+            // chains end the launch)
             {
                 const bool avail = s.role() == ROLE_FREE && done;
                 const bool want = s.role() == ROLE_OWNER && !s.hasp() && left > 0;
-                const unsigned long long fm = __ballot(avail), om = __ballot(want);
-                if (fm && om) {
-                    const uint32_t k = min((uint32_t)__popcll(fm), (uint32_t)__popcll(om));
+                const unsigned long long fm = __ballot(avail), owm = __ballot(want);
+                if (fm && owm) {
+                    uint32_t ml = want ? left : 0u;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) ml = max(ml, (uint32_t)__shfl_xor((int)ml, o));
+                    const bool t1 = want && 2u * left >= ml;
+                    const unsigned long long om1 = __ballot(t1), om2 = owm & ~om1;
+                    const uint32_t nf = (uint32_t)__popcll(fm);
+                    const uint32_t k1 = min(nf, (uint32_t)__popcll(om1));
+                    const uint32_t k2 = min(nf - k1, (uint32_t)__popcll(om2));
                     if (avail) {
                         const uint32_t fr = lane_prefix(fm);
-                        if (fr < k) {
+                        if (fr < k1 + k2) {
                             s.set(SpecState::ROLE, 2, ROLE_HELPER);
-                            s.set(SpecState::PART, 6, (uint32_t)nth_set_bit(om, fr));
+                            s.set(SpecState::PART, 6, (uint32_t)(fr < k1 ? nth_set_bit(om1, fr) : nth_set_bit(om2, fr - k1)));
                             s.set(SpecState::HASP, 1, 1);
                         }
                     }
                     if (want) {
-                        const uint32_t orank = lane_prefix(om);
-                        if (orank < k) {
-                            s.set(SpecState::PART, 6, (uint32_t)nth_set_bit(fm, orank));
+                        const uint32_t orank = t1 ? lane_prefix(om1) : lane_prefix(om2);
+                        if (orank < (t1 ? k1 : k2)) {
+                            s.set(SpecState::PART, 6, (uint32_t)nth_set_bit(fm, t1 ? orank : k1 + orank));
                             s.set(SpecState::HASP, 1, 1);
                         }
                     }
