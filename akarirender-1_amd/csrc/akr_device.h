@@ -278,6 +278,7 @@ struct PathProfile {
     unsigned long long t_max;      // longest wave (atomicMax)
     unsigned long long lanes_proc; // waiting lanes processed, summed over phases
     unsigned long long t_shade;    // ticks of A spent on finished rays' results (shading, shadow hand-over)
+    unsigned long long spec_started, spec_aborted;  // k_path_spec: speculative samples started / dropped
 };
 
 // Persistent path kernel (k_path): the whole sample loop of every pixel of the tile list.

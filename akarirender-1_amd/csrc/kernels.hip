@@ -2323,6 +2323,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     bool done = false, fin = false, busy = false;
     uint32_t idle_rounds = 0;
     uint32_t pc_closest = 0, pc_shadow = 0, sc_closest = 0, sc_shadow = 0;  // counting build: pixel / sample rays
+    unsigned long long n_spec = 0, n_abort = 0;                              // counting build: speculation
     PathRay r{};
     r.best = kInf;
     r.bgid = kNoHit;
@@ -2479,6 +2480,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     }
                 }
                 if (abort_self) {  // a dropped speculation: its ray (in flight or fresh) goes with it
+                    if (COUNT) n_abort++;
                     s.set(SpecState::SRUN, 1, 0);
                     s.set(SpecState::SEND, 1, 0);
                     s.set(SpecState::PEND, 1, 0);
@@ -2552,6 +2554,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                             nif = 1;
                             s.set(SpecState::HEADH, 1, 0);
                         } else if (nif == 1 && s.headh()) {  // the helper runs the head: its successor here
+                            if (COUNT) n_spec++;
                             seed = lcg_advance(p_start, guess);
                             sstart = seed;
                             start = true;
@@ -2571,6 +2574,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const uint32_t gstate = (uint32_t)__shfl((int)hstart, part);
                 const uint32_t opix = (uint32_t)__shfl((int)pix, part);
                 if (s.role() == ROLE_HELPER && go) {
+                    if (COUNT) n_spec++;
                     seed = gstate;
                     sstart = gstate;
                     start = true;
@@ -2631,7 +2635,14 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         }
         if (COUNT) p_tl += wall_clock64() - p_t;
     }
-    if (COUNT) path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
+    if (COUNT) {
+        path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
+        const unsigned long long ns = wave_sum(n_spec), na = wave_sum(n_abort);
+        if (__lane_id() == 0 && pa.prof) {
+            atomicAdd(&pa.prof->spec_started, ns);
+            atomicAdd(&pa.prof->spec_aborted, na);
+        }
+    }
     if (pa.fault_test && pa.fault && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_or(pa.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

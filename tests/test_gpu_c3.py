@@ -226,7 +226,7 @@ def test_c3_integrator_probe_bit_exact(c3):
     # the paths really bounce and sample lights here: the fingerprint is not trivially equal
     assert opr["shadow_rays"][ys, xs].sum() > 0 and (opr["closest_rays"][ys, xs] > 2).mean() > 0.2
     counted = _render_forms(ctx, orad, ow, opr, tiles, 2, 5)
-    assert len(counted) == 6, counted
+    assert len(counted) == 8, counted
 
 
 LIT_CAMERA = dict(position=(0.0, 1.4, 1.6), rotation=(0.0, -40.0, 0.0), fov=70.0)
@@ -249,7 +249,7 @@ def test_c3_lit_view_render_bit_exact(c3):
         L = orad.sum(-1)[sel] / 2
         assert L.mean() > 0.2 and (L > 0).mean() > 0.15, f"view not lit: mean {L.mean()}, lit {(L > 0).mean()}"
         counted = _render_forms(ctx, orad, ow, opr, tiles, 2, 5)
-        assert len(counted) == 6, counted
+        assert len(counted) == 8, counted
     finally:
         c = cs.camera
         ctx.set_camera(c.position, c.rotation, c.fov, c.resolution)

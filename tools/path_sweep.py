@@ -132,7 +132,9 @@ def main():
                                   f"(results/shading {us(q['t_shade']) / max(1, q['procs']):.2f}), "
                                   f"per outer leaf {us(q['t_leaf']) / max(1, q['outer']):.3f}; rays/px closest "
                                   f"{c['per_mode']['closest']['rays'] / n / args.steps:.2f} shadow "
-                                  f"{c['per_mode']['shadow']['rays'] / n / args.steps:.2f}", flush=True)
+                                  f"{c['per_mode']['shadow']['rays'] / n / args.steps:.2f}; speculative samples "
+                                  f"{q['spec_started'] / n / args.steps:.3f} per sample, dropped "
+                                  f"{q['spec_aborted'] / max(1, q['spec_started']):.3f}", flush=True)
             ctx.close()
 
 
