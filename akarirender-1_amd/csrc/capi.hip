@@ -260,9 +260,12 @@ struct akr_hip_ctx {
     int path_defer = 2;
     // option "path_spec": k_path_spec (lanes left idle by the drained pixel queue run
     // the next sample of a busy pixel from a guessed sampler state; committed in order, bit-exact):
-    // 1 = always, 0 = never, 2 = for renders of at most path_spec_pixels pixels
-    int path_spec = 0;
-    int64_t path_spec_pixels = 600000;
+    // 1 = always, 0 = never, 2 (default) = for renders of at most path_spec_pixels pixels of scenes of at
+    // least path_defer_min_tris triangles, where it replaces k_path_defer (measured on C3 at 1040 spp:
+    // 8-way share 0.89 -> 0.83 ms per spp, 2-way 2.55 -> 2.48, 4-way unchanged, the whole frame 2 %
+    // slower, profiles/r19_spec_ab.log)
+    int path_spec = 2;
+    int64_t path_spec_pixels = 1200000;
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
@@ -993,7 +996,8 @@ struct akr_hip_ctx {
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels &&
                                                         (int64_t)n_tris() >= path_defer_min_tris));
                 // speculative samples on the lanes a drained queue leaves idle
-                const bool spec = path_spec == 1 || (path_spec == 2 && (int64_t)N <= path_spec_pixels);
+                const bool spec = path_spec == 1 || (path_spec == 2 && (int64_t)N <= path_spec_pixels &&
+                                                     (int64_t)n_tris() >= path_defer_min_tris);
                 const int kind = spec ? PATH_SPEC : (defer ? PATH_DEFER : PATH_PLAIN);
                 // the shading's material / light / CDF tables in LDS when they fit
                 const bool tab = path_tab && path_tab_fits(n_mats, n_lights);

@@ -544,7 +544,7 @@ def main():
     # untimed same-run leg in north_star's layout (wavefront: raygen -> closest -> shade -> shadow
     # -> splat launches per bounce), when the timed render ran a persistent kernel
     wavefront = None
-    if rank == 0 and args.wavefront_spp > 0 and form["form"] in ("k_path", "k_path_defer"):
+    if rank == 0 and args.wavefront_spp > 0 and form["form"] in ("k_path", "k_path_defer", "k_path_spec"):
         # the plain wavefront (no lookahead lanes), whatever options the timed render ran with;
         # the options in effect before are restored afterwards
         saved = {k: ctx.option_set(k) for k in ("stats", "path", "lookahead")}

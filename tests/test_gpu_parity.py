@@ -588,8 +588,11 @@ def test_auto_form_by_shading(hip_ctx_factory):
                 assert set(ctx.kernel_stats()) == {want}, (sc, complex_ok, ctx.kernel_stats())
                 # a 36-triangle scene takes k_path even at a small pixel count (path_defer_min_tris)
                 assert ctx.render_form()["form"] == ("k_path" if (simple or complex_ok) else "wavefront")
-    with hip_ctx_factory(0) as ctx:   # >= 10K triangles at <= 600K pixels: the deferred form
+    with hip_ctx_factory(0) as ctx:   # >= 10K triangles at <= 1.2 M pixels: the speculative form
         cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
+        _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
+        assert ctx.render_form() == {"form": "k_path_spec", "ordered": False}
+        ctx.set_option("path_spec", 0)    # without it, the deferred form (<= 600K pixels)
         _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
         assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
         # the cost-ordered fetch from path_order_min_spp (16) samples
