@@ -2253,28 +2253,35 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #undef DEFER_SPLAT
 
 // ------------------------------------------------------------- persistent path, speculative samples
-// k_path_spec: k_path whose lanes, once the pixel queue is drained, run the NEXT
-// sample of a busy pixel of their wave speculatively.  A pixel's samples are sequential only
-// through its sampler state (cpu/integrator.cpp:124-134): sample s + 1 starts where sample s
-// stopped drawing, 4 + 6 k draws later for k scattering events (pathtracer.h:96-164).  The helper
-// starts sample s + 1 from the guessed state lcg_advance(start(s), g) with g = 4 + 6 max_depth (a
-// full-length path: on the C3 soup the costliest pixels' samples are full length 91-100 % of the
-// time, tools/sample_lengths.py), while the pixel's owner runs sample s.  Samples are committed in
-// order by the owner: the head (the one that started from the committed state C) is added to the
-// film and C becomes its end state E; the other sample is kept iff it started from exactly E (it is
-// then the sequential sample s + 1, bit for bit), otherwise it is dropped and rerun.  So the film
-// sums and the final sampler state are the sequential loop's.  At most two samples of a pixel are
-// in flight (its head and one successor), on the owner's lane and its helper's.  Every hand-off is a
-// lane shuffle inside one wave.
+// k_path_spec: k_path whose lanes, once the pixel queue is drained, help a busy
+// pixel of their wave by running its later samples speculatively.  A pixel's samples are
+// sequential only through its sampler state (cpu/integrator.cpp:124-134): sample s + 1 starts where
+// sample s stopped drawing, 4 + 6 k draws later for k scattering events (pathtracer.h:96-164).
+// A pixel is run by two lanes, its owner (which holds the pixel, its film sums and the committed
+// state C) and a helper.  The "head" lane runs the sample that starts from C; the other ("tail")
+// lane runs the next sample from the guessed state lcg_advance(start(head), g) with g = 4 + 6
+// max_depth (a full-length path: on the C3 soup the costliest pixels' samples are full length
+// 91-100 % of the time, tools/sample_lengths.py).  A tail sample that ends before the head is held
+// (its L and end state in registers) and the tail continues with the sample after it, which starts
+// from the held end state (no further guess).  The owner commits in order: the head's L is added to
+// the film and C becomes its end state E; the tail's first sample is kept iff it started from
+// exactly E (the guess was the true sample boundary: it is then the sequential sample, bit for bit),
+// and with it the sample after it; otherwise both are dropped and rerun.  The lanes then swap head
+// and tail.  So the film sums (Tile::add_sample in sample order, core/film.h:66-70) and the final
+// sampler state are the sequential loop's.  At most three samples of a pixel are in flight.  Every
+// hand-off is a lane shuffle inside one wave.
 enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
-enum : uint32_t { CMD_NONE = 0, CMD_CONSUMED = 1, CMD_ABORT = 2, CMD_RELEASE = 3 };
+// owner -> helper commands (a bit set)
+enum : uint32_t { CMD_CONS_CUR = 1, CMD_CONS_HELD = 2, CMD_ABORT = 4, CMD_RELEASE = 8, CMD_GUESS = 16, CMD_HOLD = 32 };
 
 struct SpecState {
     uint32_t w = 0;
     // ROLE: free / owner / helper; PART: the partner lane (owner: its helper, helper: its owner) when
-    // HASP; SRUN: the lane runs a sample; SEND: its sample ended, (Lr, seed) wait to be committed;
-    // HEADH (owner): the helper's sample is the head; NIF (owner): the pixel's samples in flight
-    static constexpr uint32_t ROLE = 0, PART = 2, HASP = 8, SRUN = 9, SEND = 10, HEADH = 11, NIF = 12, ANY = 14, PEND = 15;
+    // HASP; SRUN: the lane's current sample runs; SEND: it ended, (Lr, seed) wait to be committed;
+    // HELD: the lane holds a finished earlier sample (hL, hE); HEADH (owner): the helper is the head
+    // lane; NIF (owner): the pixel's samples in flight (0..3)
+    static constexpr uint32_t ROLE = 0, PART = 2, HASP = 8, SRUN = 9, SEND = 10, HELD = 11, HEADH = 12, NIF = 13,
+                              ANY = 15, PEND = 16;
     __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
     __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
         const uint32_t m = ((1u << bits) - 1u) << off;
@@ -2285,6 +2292,7 @@ struct SpecState {
     __device__ __forceinline__ bool hasp() const { return get(HASP, 1) != 0; }
     __device__ __forceinline__ bool srun() const { return get(SRUN, 1) != 0; }
     __device__ __forceinline__ bool send() const { return get(SEND, 1) != 0; }
+    __device__ __forceinline__ bool held() const { return get(HELD, 1) != 0; }
     __device__ __forceinline__ bool headh() const { return get(HEADH, 1) != 0; }
     __device__ __forceinline__ uint32_t nif() const { return get(NIF, 2); }
     __device__ __forceinline__ bool any() const { return get(ANY, 1) != 0; }
@@ -2312,18 +2320,19 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     f.s_lo = shard_begin(n, f.shard);
     f.s_hi = shard_begin(n, f.shard + 1);
 
-    // owner: its pixel, the samples not yet started, the film sums; every lane: the sample it runs
-    uint32_t pix = 0, left = 0, seed = 0, sstart = 0;
+    // owner: its pixel, the samples not yet started, the film sums, the guessed start of the tail's
+    // first sample; every lane: the sample it runs (seed, sstart, ...) and one held finished sample
+    uint32_t pix = 0, left = 0, seed = 0, sstart = 0, gst = 0, hE = 0;
     int depth = 0;
-    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f};
-    float4 film = {0.0f, 0.0f, 0.0f, 0.0f};
+    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f}, hL{0.0f, 0.0f, 0.0f};
     float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
     SpecState s;
     s.set(SpecState::PART, 6, lane);
     bool done = false, fin = false, busy = false;
     uint32_t idle_rounds = 0;
-    uint32_t pc_closest = 0, pc_shadow = 0, sc_closest = 0, sc_shadow = 0;  // counting build: pixel / sample rays
-    unsigned long long n_spec = 0, n_abort = 0;                              // counting build: speculation
+    // counting build: the pixel's committed rays; the current and the held sample's rays
+    uint32_t pc_closest = 0, pc_shadow = 0, sc_closest = 0, sc_shadow = 0, hc_closest = 0, hc_shadow = 0;
+    unsigned long long n_spec = 0, n_abort = 0;
     PathRay r{};
     r.best = kInf;
     r.bgid = kNoHit;
@@ -2408,57 +2417,91 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 }
             }
             if (COUNT) p_tsh += wall_clock64() - p_ts;
-            // 2. owners commit their samples in order; every lane reads its partner's sample
+            // 2. owners commit their pixel's samples in order, reading the helper's lane
             {
                 const int part = (int)s.part();
-                const uint32_t p_send = (uint32_t)__shfl((int)s.get(SpecState::SEND, 1), part);
-                const uint32_t p_start = (uint32_t)__shfl((int)sstart, part);
+                const uint32_t p_w = (uint32_t)__shfl((int)s.w, part);
                 const uint32_t p_end = (uint32_t)__shfl((int)seed, part);
-                V3 p_L;
+                const uint32_t p_hE = (uint32_t)__shfl((int)hE, part);
+                V3 p_L, p_hL;
                 p_L.x = __shfl(Lr.x, part);
                 p_L.y = __shfl(Lr.y, part);
                 p_L.z = __shfl(Lr.z, part);
-                uint32_t p_cc = 0, p_cs = 0;
+                p_hL.x = __shfl(hL.x, part);
+                p_hL.y = __shfl(hL.y, part);
+                p_hL.z = __shfl(hL.z, part);
+                uint32_t p_cc = 0, p_cs = 0, p_hcc = 0, p_hcs = 0;
                 if (COUNT) {
                     p_cc = (uint32_t)__shfl((int)sc_closest, part);
                     p_cs = (uint32_t)__shfl((int)sc_shadow, part);
+                    p_hcc = (uint32_t)__shfl((int)hc_closest, part);
+                    p_hcs = (uint32_t)__shfl((int)hc_shadow, part);
                 }
-                uint32_t cmd = CMD_NONE;
+                SpecState ps;
+                ps.w = p_w;
+                uint32_t cmd = 0;
                 if (s.role() == ROLE_OWNER) {
                     uint32_t nif = s.nif();
-                    for (int it = 0; it < 2 && nif > 0; it++) {
+                    bool p_send = ps.send(), p_held = ps.held();
+                    // the pixel's film sums live in its film slot (zeroed by the render's setup), read
+                    // and written around the commits (registers are the limit here)
+                    const bool commits = nif > 0 && (s.headh() ? p_send : s.send());
+                    float4 film = commits ? pa.film[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    for (int it = 0; it < 3 && nif > 0; it++) {
                         const bool headh = s.headh();
-                        if (!(headh ? p_send != 0 : s.send())) break;
+                        if (!(headh ? p_send : s.send())) break;
+                        // the head lane's current sample: Tile::add_sample, C = its end state
                         const V3 L = headh ? p_L : Lr;
-                        const uint32_t E = headh ? p_end : seed;
-                        splat_one(film, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);  // Tile::add_sample
+                        uint32_t E = headh ? p_end : seed;
+                        splat_one(film, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
                         if (COUNT) {
                             pc_closest += headh ? p_cc : sc_closest;
                             pc_shadow += headh ? p_cs : sc_shadow;
                         }
-                        if (headh) cmd = CMD_CONSUMED;
-                        else s.set(SpecState::SEND, 1, 0);
+                        if (headh) {
+                            cmd |= CMD_CONS_CUR;
+                            p_send = false;
+                        } else {
+                            s.set(SpecState::SEND, 1, 0);
+                        }
                         nif--;
-                        if (nif == 1) {  // the other sample is the next one iff it started from E
-                            const uint32_t o_start = headh ? sstart : p_start;
-                            if (o_start == E) {
-                                s.set(SpecState::HEADH, 1, headh ? 0u : 1u);
-                                continue;
+                        if (nif > 0) {
+                            // the tail's first sample is the next one iff its guessed start is E
+                            if (gst != E) {
+                                if (headh) abort_self = true;
+                                else cmd |= CMD_ABORT;
+                                left += nif;
+                                nif = 0;
+                            } else {
+                                s.set(SpecState::HEADH, 1, headh ? 0u : 1u);  // the tail is the head lane now
+                                const bool t_held = headh ? s.held() : p_held;
+                                if (t_held) {  // its held sample is committed at once
+                                    const V3 HL = headh ? hL : p_hL;
+                                    E = headh ? hE : p_hE;
+                                    splat_one(film, make_float4(HL.x, HL.y, HL.z, 0.0f), pa.ray_clamp);
+                                    if (COUNT) {
+                                        pc_closest += headh ? hc_closest : p_hcc;
+                                        pc_shadow += headh ? hc_shadow : p_hcs;
+                                    }
+                                    if (headh) s.set(SpecState::HELD, 1, 0);
+                                    else {
+                                        cmd |= CMD_CONS_HELD;
+                                        p_held = false;
+                                    }
+                                    nif--;
+                                }
+                                if (nif > 0) continue;  // its current sample started from E: the head
                             }
-                            if (headh) abort_self = true;  // the owner's own successor
-                            else cmd = CMD_ABORT;
-                            left++;
-                            nif = 0;
                         }
                         seed = E;  // nothing in flight: the owner's lane holds the committed state
                     }
                     s.set(SpecState::NIF, 2, nif);
-                    if (nif == 0 && left == 0 && !s.srun() && !s.send()) {  // the pixel is done
-                        pa.film[pix] = film;
+                    if (commits) pa.film[pix] = film;
+                    if (nif == 0 && left == 0) {  // the pixel is done
                         if (pa.probe)
                             pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
                                                        COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
-                        if (s.hasp()) cmd = CMD_RELEASE;
+                        if (s.hasp()) cmd |= CMD_RELEASE;
                         s.set(SpecState::ROLE, 2, ROLE_FREE);
                         s.set(SpecState::HASP, 1, 0);
                         s.set(SpecState::PART, 6, lane);
@@ -2467,22 +2510,20 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 // 3. helpers apply their owner's decision
                 const uint32_t hcmd = (uint32_t)__shfl((int)cmd, part);
                 if (s.role() == ROLE_HELPER) {
-                    if (hcmd == CMD_CONSUMED) {
-                        s.set(SpecState::SEND, 1, 0);
-                    } else if (hcmd == CMD_ABORT) {
-                        abort_self = true;
-                    } else if (hcmd == CMD_RELEASE) {  // the pixel is done: nothing of it is in flight
+                    if (hcmd & CMD_CONS_CUR) s.set(SpecState::SEND, 1, 0);
+                    if (hcmd & CMD_CONS_HELD) s.set(SpecState::HELD, 1, 0);
+                    if (hcmd & CMD_ABORT) abort_self = true;
+                    if (hcmd & CMD_RELEASE) {  // the pixel is done: nothing of it is in flight
                         s.set(SpecState::ROLE, 2, ROLE_FREE);
                         s.set(SpecState::HASP, 1, 0);
                         s.set(SpecState::PART, 6, lane);
-                        s.set(SpecState::SRUN, 1, 0);
-                        s.set(SpecState::SEND, 1, 0);
                     }
                 }
-                if (abort_self) {  // a dropped speculation: its ray (in flight or fresh) goes with it
+                if (abort_self) {  // a dropped speculation: its samples and its ray go with it
                     if (COUNT) n_abort++;
                     s.set(SpecState::SRUN, 1, 0);
                     s.set(SpecState::SEND, 1, 0);
+                    s.set(SpecState::HELD, 1, 0);
                     s.set(SpecState::PEND, 1, 0);
                     fresh = false;
                     busy = false;
@@ -2497,7 +2538,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     const uint32_t px = pa.pixel[pix];
                     left = pa.spp;
                     seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
-                    film = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                     s.set(SpecState::ROLE, 2, ROLE_OWNER);
                     s.set(SpecState::NIF, 2, 0);
                     s.set(SpecState::HEADH, 1, 0);
@@ -2537,50 +2577,72 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     }
                 }
             }
-            // 6. the owner starts samples: its head from C, or the successor of the head from the
-            // guessed state, on its own lane and on its helper's
+            // 6. the owner starts samples: the head from C when nothing is in flight; on the tail lane,
+            // the sample after the head from the guessed state, or, when the tail's sample ended before
+            // the head, it is held and the tail goes on with the sample after it
             {
                 const int part = (int)s.part();
-                const uint32_t p_idle = (uint32_t)__shfl((int)((s.srun() || s.send()) ? 0u : 1u), part);
+                SpecState ps;
+                ps.w = (uint32_t)__shfl((int)s.w, part);
                 const uint32_t p_start = (uint32_t)__shfl((int)sstart, part);
-                uint32_t hstart = 0, hgo = 0;
+                uint32_t hcmd = 0;
+                bool self_guess = false, self_hold = false;
                 if (s.role() == ROLE_OWNER) {
                     uint32_t nif = s.nif();
-                    if (!s.srun() && !s.send() && left > 0) {
-                        if (nif == 0) {  // the head, from the committed state
-                            sstart = seed;
-                            start = true;
-                            left--;
-                            nif = 1;
-                            s.set(SpecState::HEADH, 1, 0);
-                        } else if (nif == 1 && s.headh()) {  // the helper runs the head: its successor here
-                            if (COUNT) n_spec++;
-                            seed = lcg_advance(p_start, guess);
-                            sstart = seed;
-                            start = true;
+                    if (nif == 0 && left > 0) {  // the head, from the committed state, on the owner's lane
+                        start = true;
+                        left--;
+                        nif = 1;
+                        s.set(SpecState::HEADH, 1, 0);
+                    }
+                    const bool headh = s.headh();
+                    const bool have_tail = headh || s.hasp();  // the tail lane: the owner's or the helper's
+                    if (nif >= 1 && left > 0 && have_tail) {
+                        const bool t_run = headh ? s.srun() : ps.srun();
+                        const bool t_end = headh ? s.send() : ps.send();
+                        const bool t_held = headh ? s.held() : ps.held();
+                        if (nif == 1 && !t_run && !t_end && !t_held) {  // the tail's first sample, guessed
+                            // the head's start: the helper's, or the owner's (just set when it started now)
+                            gst = lcg_advance(headh ? p_start : (start ? seed : sstart), guess);
+                            if (headh) self_guess = true;
+                            else hcmd = CMD_GUESS;
                             left--;
                             nif = 2;
+                        } else if (nif == 2 && t_end && !t_held) {  // hold it and go on with the next
+                            if (headh) self_hold = true;
+                            else hcmd = CMD_HOLD;
+                            left--;
+                            nif = 3;
                         }
-                    }
-                    if (s.hasp() && p_idle && left > 0 && nif == 1 && !s.headh()) {  // successor on the helper
-                        hstart = lcg_advance(sstart, guess);
-                        hgo = 1;
-                        left--;
-                        nif = 2;
                     }
                     s.set(SpecState::NIF, 2, nif);
                 }
-                const uint32_t go = (uint32_t)__shfl((int)hgo, part);
-                const uint32_t gstate = (uint32_t)__shfl((int)hstart, part);
+                const uint32_t go = (uint32_t)__shfl((int)hcmd, part);
+                const uint32_t gstate = (uint32_t)__shfl((int)gst, part);
                 const uint32_t opix = (uint32_t)__shfl((int)pix, part);
-                if (s.role() == ROLE_HELPER && go) {
+                if (s.role() == ROLE_HELPER) {
+                    self_guess = go == CMD_GUESS;
+                    self_hold = go == CMD_HOLD;
+                }
+                if (self_guess) {  // from the guessed state (the owner's gst)
                     if (COUNT) n_spec++;
-                    seed = gstate;
-                    sstart = gstate;
+                    seed = s.role() == ROLE_HELPER ? gstate : gst;
+                    start = true;
+                }
+                if (self_hold) {  // keep the finished sample, the next one starts from its end state
+                    hL = Lr;
+                    hE = seed;
+                    if (COUNT) {
+                        hc_closest = sc_closest;
+                        hc_shadow = sc_shadow;
+                    }
+                    s.set(SpecState::HELD, 1, 1);
+                    s.set(SpecState::SEND, 1, 0);
                     start = true;
                 }
                 if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
                     const uint32_t px = pa.pixel[s.role() == ROLE_HELPER ? opix : pix];
+                    sstart = seed;
                     Lr = V3{0.0f, 0.0f, 0.0f};
                     beta = V3{1.0f, 1.0f, 1.0f};
                     depth = 0;
