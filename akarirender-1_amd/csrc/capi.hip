@@ -167,6 +167,7 @@ struct akr_hip_ctx {
     // Test-only per-slot fingerprint of the last render (option "pixel_probe", akr_pixel_probe)
     bool probe = false;
     bool fault_test = false;  // option "fault_test": k_path_defer raises the fault word once (tests)
+    bool probe_clock = false; // option "pixel_probe" 2: completion times in the probe (counting build, diagnostic)
     DBuf<uint4> d_probe;
     uint64_t probe_n = 0;
     bool probe_ok = false;
@@ -992,6 +993,7 @@ struct akr_hip_ctx {
                 pa.probe = probe_p;
                 pa.fault = d_fault_host;
                 pa.fault_test = fault_test ? 1u : 0u;
+                pa.probe_clock = probe_clock ? 1u : 0u;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels &&
                                                         (int64_t)n_tris() >= path_defer_min_tris));
@@ -1376,6 +1378,7 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_min_wait = (int)value;
         } else if (k == "pixel_probe") {
             ctx->probe = value != 0;
+            ctx->probe_clock = value == 2;
         } else if (k == "fault_test") {
             ctx->fault_test = value != 0;
         } else if (k == "verify") {

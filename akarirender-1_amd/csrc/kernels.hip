@@ -1689,6 +1689,16 @@ __device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &
 // and stack pointer stay in registers across the processing phase, where the waiting lanes read
 // their finished ray's hit.  Parking all 14 words measured 4.5 % slower: the 6 KB
 // per workgroup it takes holds three more stack entries per lane.
+// The probe record's flags (akr_pixel_probe): the seed always, the ray counts in the counting
+// build, and with option "pixel_probe" 2 the pixel's completion time (wall clock / 16 above bit 8)
+template <bool COUNT>
+__device__ __forceinline__ uint32_t probe_flags(const PathArgs &pa) {
+    if (!COUNT) return AKR_PROBE_SEED;
+    uint32_t f = AKR_PROBE_SEED | AKR_PROBE_RAYS;
+    if (pa.probe_clock) f |= 4u | (uint32_t)((wall_clock64() >> 4) << 8);
+    return f;
+}
+
 constexpr int kParkSlots = 8;
 
 template <bool COUNT, bool TAB>
@@ -1818,7 +1828,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     pa.film[pix] = film;
                     if (pa.probe)
                         pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
-                                                   COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
+                                                   probe_flags<COUNT>(pa));
                     need_pixel = true;
                 } else {
                     start = true;
@@ -2136,7 +2146,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             if (free_lane && !done && !need_pixel && !s.running() && left == 0 && s.open() == 0) {
                 if (pa.probe)
                     pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
-                                               COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
+                                               probe_flags<COUNT>(pa));
                 need_pixel = true;
             }
             const bool asked = need_pixel && !done;
@@ -2500,7 +2510,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     if (nif == 0 && left == 0) {  // the pixel is done
                         if (pa.probe)
                             pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
-                                                       COUNT ? AKR_PROBE_SEED | AKR_PROBE_RAYS : AKR_PROBE_SEED);
+                                                       probe_flags<COUNT>(pa));
                         if (s.hasp()) cmd |= CMD_RELEASE;
                         s.set(SpecState::ROLE, 2, ROLE_FREE);
                         s.set(SpecState::HASP, 1, 0);
