@@ -2263,50 +2263,45 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #undef DEFER_SPLAT
 
 // ------------------------------------------------------------- persistent path, speculative samples
-// k_path_spec: k_path whose lanes, once the pixel queue is drained, help a busy
-// pixel of their wave by running its later samples speculatively.  A pixel's samples are
+// k_path_spec: k_path whose lanes, once the pixel queue is drained, help the busy
+// pixels of their wave by running their later samples speculatively.  A pixel's samples are
 // sequential only through its sampler state (cpu/integrator.cpp:124-134): sample s + 1 starts where
 // sample s stopped drawing, 4 + 6 k draws later for k scattering events (pathtracer.h:96-164).
-// A pixel is run by two lanes, its owner (which holds the pixel, its film sums and the committed
-// state C) and a helper.  The "head" lane runs the sample that starts from C; the other ("tail")
-// lane runs the next sample from the guessed state lcg_advance(start(head), g) with g = 4 + 6
-// max_depth (a full-length path: on the C3 soup the costliest pixels' samples are full length
-// 91-100 % of the time, tools/sample_lengths.py).  A tail sample that ends before the head is held
-// (its L and end state in registers) and the tail continues with the sample after it, which starts
-// from the held end state (no further guess).  The owner commits in order: the head's L is added to
-// the film and C becomes its end state E; the tail's first sample is kept iff it started from
-// exactly E (the guess was the true sample boundary: it is then the sequential sample, bit for bit),
-// and with it the sample after it; otherwise both are dropped and rerun.  The lanes then swap head
-// and tail.  So the film sums (Tile::add_sample in sample order, core/film.h:66-70) and the final
-// sampler state are the sequential loop's.  At most three samples of a pixel are in flight.  Every
-// hand-off is a lane shuffle inside one wave.
+// A pixel is run by a group of lanes: its owner (the pixel, its film slot, the committed state C,
+// the samples not yet started) and up to kSpecHelpers helpers.  The samples in flight are numbered
+// (seq); the one numbered like the next commit (cseq) is the head.  A new sample starts from C when
+// it is the head, otherwise from the guessed state lcg_advance(start(previous sample), g) with
+// g = 4 + 6 max_depth (a full-length path: on the C3 soup the costliest pixels' samples are full
+// length 91-100 % of the time, tools/sample_lengths.py), so the k-th sample ahead is k guesses deep.
+// The owner commits in order: a finished head whose start is C is added to the film
+// (Tile::add_sample, core/film.h:66-70) and C becomes its end state; a head whose start is not C
+// was guessed wrong, and every sample in flight is dropped (a new generation) and rerun.  So the
+// film sums and the final sampler state are the sequential loop's, bit for bit.  The lanes of a
+// group find each other with wave ballots against the owner's group mask; every hand-off is a lane
+// shuffle inside one wave.
+constexpr uint32_t kSpecHelpers = 15;   // helpers per pixel (a group spans at most 16 lanes)
 enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
-// owner -> helper commands (a bit set)
-enum : uint32_t { CMD_CONS_CUR = 1, CMD_CONS_HELD = 2, CMD_ABORT = 4, CMD_RELEASE = 8, CMD_GUESS = 16, CMD_HOLD = 32 };
 
 struct SpecState {
     uint32_t w = 0;
-    // ROLE: free / owner / helper; PART: the partner lane (owner: its helper, helper: its owner) when
-    // HASP; SRUN: the lane's current sample runs; SEND: it ended, (Lr, seed) wait to be committed;
-    // HELD: the lane holds a finished earlier sample (hL, hE); HEADH (owner): the helper is the head
-    // lane; NIF (owner): the pixel's samples in flight (0..3)
-    static constexpr uint32_t ROLE = 0, PART = 2, HASP = 8, SRUN = 9, SEND = 10, HELD = 11, HEADH = 12, NIF = 13,
-                              ANY = 15, PEND = 16;
+    // ROLE: free / owner / helper; OL: a helper's owner lane; SRUN: the lane's sample runs; SEND: it
+    // ended, (Lr, seed) wait for the commit; NIF (owner): samples in flight; NH (owner): helpers;
+    // GEN (owner): the generation of its samples in flight
+    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NIF = 12, NH = 17, GEN = 22;
     __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
     __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
         const uint32_t m = ((1u << bits) - 1u) << off;
         w = (w & ~m) | ((v << off) & m);
     }
     __device__ __forceinline__ uint32_t role() const { return get(ROLE, 2); }
-    __device__ __forceinline__ uint32_t part() const { return get(PART, 6); }
-    __device__ __forceinline__ bool hasp() const { return get(HASP, 1) != 0; }
+    __device__ __forceinline__ uint32_t ol() const { return get(OL, 6); }
     __device__ __forceinline__ bool srun() const { return get(SRUN, 1) != 0; }
     __device__ __forceinline__ bool send() const { return get(SEND, 1) != 0; }
-    __device__ __forceinline__ bool held() const { return get(HELD, 1) != 0; }
-    __device__ __forceinline__ bool headh() const { return get(HEADH, 1) != 0; }
-    __device__ __forceinline__ uint32_t nif() const { return get(NIF, 2); }
     __device__ __forceinline__ bool any() const { return get(ANY, 1) != 0; }
     __device__ __forceinline__ bool pend() const { return get(PEND, 1) != 0; }
+    __device__ __forceinline__ uint32_t nif() const { return get(NIF, 5); }
+    __device__ __forceinline__ uint32_t nh() const { return get(NH, 5); }
+    __device__ __forceinline__ uint32_t gen() const { return get(GEN, 10); }
 };
 
 template <bool COUNT, bool TAB>
@@ -2320,6 +2315,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const uint32_t tid = threadIdx.x;
     const uint32_t gtid = blockIdx.x * kTraceBlock + tid;
     const uint32_t lane = __lane_id();
+    const unsigned long long below = (1ull << lane) - 1ull;  // lanes under this one
     const uint32_t n = pa.n_pix;
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
     const uint32_t guess = 4u + 6u * (uint32_t)pa.max_depth;  // draws of a full-length sample
@@ -2330,19 +2326,20 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     f.s_lo = shard_begin(n, f.shard);
     f.s_hi = shard_begin(n, f.shard + 1);
 
-    // owner: its pixel, the samples not yet started, the film sums, the guessed start of the tail's
-    // first sample; every lane: the sample it runs (seed, sstart, ...) and one held finished sample
-    uint32_t pix = 0, left = 0, seed = 0, sstart = 0, gst = 0, hE = 0;
+    // owner: the samples not yet started, the committed state, the start of the last started sample,
+    // the next sample to commit / to start, its group's lanes; every group lane: the pixel, and the
+    // sample it runs (its state, start, number and generation)
+    uint32_t pix = 0, left = 0, C = 0, tstart = 0, cseq = 0, nseq = 0;
+    unsigned long long grp = 0;
+    uint32_t seed = 0, sstart = 0, mseq = 0, mgen = 0;
     int depth = 0;
-    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f}, hL{0.0f, 0.0f, 0.0f};
+    V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f};
     float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
     SpecState s;
-    s.set(SpecState::PART, 6, lane);
     bool done = false, fin = false, busy = false;
     uint32_t idle_rounds = 0;
-    // counting build: the pixel's committed rays; the current and the held sample's rays
-    uint32_t pc_closest = 0, pc_shadow = 0, sc_closest = 0, sc_shadow = 0, hc_closest = 0, hc_shadow = 0;
-    unsigned long long n_spec = 0, n_abort = 0;
+    uint32_t pc_closest = 0, pc_shadow = 0, sc_closest = 0, sc_shadow = 0;  // counting build: pixel / sample rays
+    unsigned long long n_spec = 0, n_abort = 0;                              // counting build: speculation
     PathRay r{};
     r.best = kInf;
     r.bgid = kNoHit;
@@ -2366,7 +2363,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             path_park(s_park, tid, r);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             asm volatile("" ::: "memory");
-            bool fresh = false, next_any = false, abort_self = false, start = false;
+            bool fresh = false, next_any = false, start = false;
             float4 ra = {}, rb = {};
             unsigned long long p_ts = 0;
             if (COUNT) p_ts = wall_clock64();
@@ -2427,119 +2424,86 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 }
             }
             if (COUNT) p_tsh += wall_clock64() - p_ts;
-            // 2. owners commit their pixel's samples in order, reading the helper's lane
-            {
-                const int part = (int)s.part();
-                const uint32_t p_w = (uint32_t)__shfl((int)s.w, part);
-                const uint32_t p_end = (uint32_t)__shfl((int)seed, part);
-                const uint32_t p_hE = (uint32_t)__shfl((int)hE, part);
-                V3 p_L, p_hL;
-                p_L.x = __shfl(Lr.x, part);
-                p_L.y = __shfl(Lr.y, part);
-                p_L.z = __shfl(Lr.z, part);
-                p_hL.x = __shfl(hL.x, part);
-                p_hL.y = __shfl(hL.y, part);
-                p_hL.z = __shfl(hL.z, part);
-                uint32_t p_cc = 0, p_cs = 0, p_hcc = 0, p_hcs = 0;
-                if (COUNT) {
-                    p_cc = (uint32_t)__shfl((int)sc_closest, part);
-                    p_cs = (uint32_t)__shfl((int)sc_shadow, part);
-                    p_hcc = (uint32_t)__shfl((int)hc_closest, part);
-                    p_hcs = (uint32_t)__shfl((int)hc_shadow, part);
-                }
-                SpecState ps;
-                ps.w = p_w;
-                uint32_t cmd = 0;
+            // 2. commits, in sample order: each group lane compares its sample with its owner's next
+            // commit; one head per group per round
+            const bool in_grp = s.role() != ROLE_FREE;
+            const int ol = s.role() == ROLE_HELPER ? (int)s.ol() : (int)lane;
+            for (int it = 0; it <= (int)kSpecHelpers; it++) {
+                const uint32_t o_cseq = (uint32_t)__shfl((int)cseq, ol);
+                const uint32_t o_C = (uint32_t)__shfl((int)C, ol);
+                SpecState os;
+                os.w = (uint32_t)__shfl((int)s.w, ol);
+                const bool mine = in_grp && (s.srun() || s.send()) && mgen == os.gen();
+                const bool head = mine && mseq == o_cseq;
+                const bool bad = head && sstart != o_C;      // a wrong guess reached the head
+                const bool ready = head && !bad && s.send();  // a finished head: commit it
+                const unsigned long long badm = __ballot(bad), rdm = __ballot(ready);
+                if ((badm | rdm) == 0) break;
+                int hl = (int)lane;
+                bool commit = false, drop = false;
                 if (s.role() == ROLE_OWNER) {
-                    uint32_t nif = s.nif();
-                    bool p_send = ps.send(), p_held = ps.held();
-                    // the pixel's film sums live in its film slot (zeroed by the render's setup), read
-                    // and written around the commits (registers are the limit here)
-                    const bool commits = nif > 0 && (s.headh() ? p_send : s.send());
-                    float4 film = commits ? pa.film[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    for (int it = 0; it < 3 && nif > 0; it++) {
-                        const bool headh = s.headh();
-                        if (!(headh ? p_send : s.send())) break;
-                        // the head lane's current sample: Tile::add_sample, C = its end state
-                        const V3 L = headh ? p_L : Lr;
-                        uint32_t E = headh ? p_end : seed;
-                        splat_one(film, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
-                        if (COUNT) {
-                            pc_closest += headh ? p_cc : sc_closest;
-                            pc_shadow += headh ? p_cs : sc_shadow;
-                        }
-                        if (headh) {
-                            cmd |= CMD_CONS_CUR;
-                            p_send = false;
-                        } else {
-                            s.set(SpecState::SEND, 1, 0);
-                        }
-                        nif--;
-                        if (nif > 0) {
-                            // the tail's first sample is the next one iff its guessed start is E
-                            if (gst != E) {
-                                if (headh) abort_self = true;
-                                else cmd |= CMD_ABORT;
-                                left += nif;
-                                nif = 0;
-                            } else {
-                                s.set(SpecState::HEADH, 1, headh ? 0u : 1u);  // the tail is the head lane now
-                                const bool t_held = headh ? s.held() : p_held;
-                                if (t_held) {  // its held sample is committed at once
-                                    const V3 HL = headh ? hL : p_hL;
-                                    E = headh ? hE : p_hE;
-                                    splat_one(film, make_float4(HL.x, HL.y, HL.z, 0.0f), pa.ray_clamp);
-                                    if (COUNT) {
-                                        pc_closest += headh ? hc_closest : p_hcc;
-                                        pc_shadow += headh ? hc_shadow : p_hcs;
-                                    }
-                                    if (headh) s.set(SpecState::HELD, 1, 0);
-                                    else {
-                                        cmd |= CMD_CONS_HELD;
-                                        p_held = false;
-                                    }
-                                    nif--;
-                                }
-                                if (nif > 0) continue;  // its current sample started from E: the head
-                            }
-                        }
-                        seed = E;  // nothing in flight: the owner's lane holds the committed state
-                    }
-                    s.set(SpecState::NIF, 2, nif);
-                    if (commits) pa.film[pix] = film;
-                    if (nif == 0 && left == 0) {  // the pixel is done
-                        if (pa.probe)
-                            pa.probe[pix] = make_uint4(seed, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u,
-                                                       probe_flags<COUNT>(pa));
-                        if (s.hasp()) cmd |= CMD_RELEASE;
-                        s.set(SpecState::ROLE, 2, ROLE_FREE);
-                        s.set(SpecState::HASP, 1, 0);
-                        s.set(SpecState::PART, 6, lane);
-                    }
+                    drop = (grp & badm) != 0;
+                    const unsigned long long m = grp & rdm;
+                    commit = !drop && m != 0;
+                    if (commit) hl = __ffsll((long long)m) - 1;
                 }
-                // 3. helpers apply their owner's decision
-                const uint32_t hcmd = (uint32_t)__shfl((int)cmd, part);
-                if (s.role() == ROLE_HELPER) {
-                    if (hcmd & CMD_CONS_CUR) s.set(SpecState::SEND, 1, 0);
-                    if (hcmd & CMD_CONS_HELD) s.set(SpecState::HELD, 1, 0);
-                    if (hcmd & CMD_ABORT) abort_self = true;
-                    if (hcmd & CMD_RELEASE) {  // the pixel is done: nothing of it is in flight
-                        s.set(SpecState::ROLE, 2, ROLE_FREE);
-                        s.set(SpecState::HASP, 1, 0);
-                        s.set(SpecState::PART, 6, lane);
-                    }
+                V3 L;
+                L.x = __shfl(Lr.x, hl);
+                L.y = __shfl(Lr.y, hl);
+                L.z = __shfl(Lr.z, hl);
+                const uint32_t E = (uint32_t)__shfl((int)seed, hl);
+                uint32_t hcc = 0, hcs = 0;
+                if (COUNT) {
+                    hcc = (uint32_t)__shfl((int)sc_closest, hl);
+                    hcs = (uint32_t)__shfl((int)sc_shadow, hl);
                 }
-                if (abort_self) {  // a dropped speculation: its samples and its ray go with it
-                    if (COUNT) n_abort++;
+                if (commit) {
+                    float4 fm = pa.film[pix];  // the film sums live in the (zeroed) film slot
+                    splat_one(fm, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
+                    pa.film[pix] = fm;
+                    if (COUNT) {
+                        pc_closest += hcc;
+                        pc_shadow += hcs;
+                    }
+                    C = E;
+                    cseq++;
+                    s.set(SpecState::NIF, 5, s.nif() - 1u);
+                } else if (drop) {  // every sample in flight: a new generation, rerun from C
+                    s.set(SpecState::GEN, 10, s.gen() + 1u);
+                    left += s.nif();
+                    nseq = cseq;
+                    s.set(SpecState::NIF, 5, 0);
+                }
+            }
+            // each group lane: its sample committed or dropped -> idle; a pixel that is done frees
+            // its group
+            {
+                if (s.role() == ROLE_OWNER && s.nif() == 0 && left == 0) {  // the pixel is done
+                    if (pa.probe)
+                        pa.probe[pix] = make_uint4(C, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u, probe_flags<COUNT>(pa));
+                    s.set(SpecState::ROLE, 2, ROLE_FREE);
+                    s.set(SpecState::NH, 5, 0);
+                    grp = 0;
+                }
+                SpecState os;
+                os.w = (uint32_t)__shfl((int)s.w, ol);
+                const uint32_t o_cseq = (uint32_t)__shfl((int)cseq, ol);
+                const uint32_t o_pix = (uint32_t)__shfl((int)pix, ol);
+                if (s.role() == ROLE_HELPER && (os.role() != ROLE_OWNER || o_pix != pix))
+                    s.set(SpecState::ROLE, 2, ROLE_FREE);  // its pixel is done (its lane may own another)
+                const bool had = s.srun() || s.send();
+                const bool gone = had && (s.role() == ROLE_FREE || mgen != os.gen() || mseq < o_cseq);
+                if (gone) {
+                    const bool committed = s.role() != ROLE_FREE && mgen == os.gen() && mseq < o_cseq;
+                    if (COUNT && !committed) n_abort++;
                     s.set(SpecState::SRUN, 1, 0);
                     s.set(SpecState::SEND, 1, 0);
-                    s.set(SpecState::HELD, 1, 0);
                     s.set(SpecState::PEND, 1, 0);
-                    fresh = false;
+                    fresh = false;  // a dropped sample's ray goes with it
                     busy = false;
                 }
             }
-            // 4. free lanes fetch the next pixel while the queue lasts
+            // 3. free lanes fetch the next pixel while the queue lasts
             {
                 bool need = s.role() == ROLE_FREE && !done;
                 const bool asked = need;
@@ -2547,20 +2511,22 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 if (asked && !need) {
                     const uint32_t px = pa.pixel[pix];
                     left = pa.spp;
-                    seed = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                    C = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                    cseq = nseq = 0;
+                    grp = 1ull << lane;
                     s.set(SpecState::ROLE, 2, ROLE_OWNER);
-                    s.set(SpecState::NIF, 2, 0);
-                    s.set(SpecState::HEADH, 1, 0);
+                    s.set(SpecState::NIF, 5, 0);
+                    s.set(SpecState::NH, 5, 0);
                     if (COUNT) pc_closest = pc_shadow = 0;
                 }
             }
-            // 5. lanes with nothing left to fetch become helpers of owners with samples to start; the
-            // owners with at least half the wave's most samples left are served first (the longest
-            // chains end the launch)
+            // 4. lanes with nothing left to fetch join the groups of owners with samples to start, one
+            // per owner per phase; the owners with at least half the wave's most samples left first
             {
                 const bool avail = s.role() == ROLE_FREE && done;
-                const bool want = s.role() == ROLE_OWNER && !s.hasp() && left > 0;
+                const bool want = s.role() == ROLE_OWNER && s.nh() < kSpecHelpers && left > 0;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
+                int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
                     uint32_t ml = want ? left : 0u;
 #pragma unroll
@@ -2572,86 +2538,63 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     const uint32_t k2 = min(nf - k1, (uint32_t)__popcll(om2));
                     if (avail) {
                         const uint32_t fr = lane_prefix(fm);
-                        if (fr < k1 + k2) {
-                            s.set(SpecState::ROLE, 2, ROLE_HELPER);
-                            s.set(SpecState::PART, 6, (uint32_t)(fr < k1 ? nth_set_bit(om1, fr) : nth_set_bit(om2, fr - k1)));
-                            s.set(SpecState::HASP, 1, 1);
-                        }
+                        if (fr < k1 + k2) nol = fr < k1 ? nth_set_bit(om1, fr) : nth_set_bit(om2, fr - k1);
                     }
                     if (want) {
                         const uint32_t orank = t1 ? lane_prefix(om1) : lane_prefix(om2);
                         if (orank < (t1 ? k1 : k2)) {
-                            s.set(SpecState::PART, 6, (uint32_t)nth_set_bit(fm, t1 ? orank : k1 + orank));
-                            s.set(SpecState::HASP, 1, 1);
+                            grp |= 1ull << nth_set_bit(fm, t1 ? orank : k1 + orank);
+                            s.set(SpecState::NH, 5, s.nh() + 1u);
                         }
                     }
+                }
+                const uint32_t np = (uint32_t)__shfl((int)pix, nol >= 0 ? nol : (int)lane);
+                if (nol >= 0) {
+                    s.set(SpecState::ROLE, 2, ROLE_HELPER);
+                    s.set(SpecState::OL, 6, (uint32_t)nol);
+                    pix = np;
                 }
             }
-            // 6. the owner starts samples: the head from C when nothing is in flight; on the tail lane,
-            // the sample after the head from the guessed state, or, when the tail's sample ended before
-            // the head, it is held and the tail goes on with the sample after it
+            // 5. starts: the idle lanes of a group take the next samples in lane order, the first from C
+            // when nothing is in flight, every other from the guessed state one full-length sample on
             {
-                const int part = (int)s.part();
-                SpecState ps;
-                ps.w = (uint32_t)__shfl((int)s.w, part);
-                const uint32_t p_start = (uint32_t)__shfl((int)sstart, part);
-                uint32_t hcmd = 0;
-                bool self_guess = false, self_hold = false;
+                const int ol2 = s.role() == ROLE_HELPER ? (int)s.ol() : (int)lane;
+                const bool idle = s.role() != ROLE_FREE && !s.srun() && !s.send();
+                const unsigned long long im = __ballot(idle);
+                uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0;
                 if (s.role() == ROLE_OWNER) {
-                    uint32_t nif = s.nif();
-                    if (nif == 0 && left > 0) {  // the head, from the committed state, on the owner's lane
+                    cnt = min((uint32_t)__popcll(grp & im), left);
+                    zero = s.nif() == 0 ? 1u : 0u;
+                    base = zero ? C : tstart;
+                    seq0 = nseq;
+                    if (cnt) {
+                        tstart = lcg_advance(base, guess * (cnt - zero));  // the last new sample's start
+                        nseq += cnt;
+                        left -= cnt;
+                        s.set(SpecState::NIF, 5, s.nif() + cnt);
+                    }
+                }
+                const uint32_t o_cnt = (uint32_t)__shfl((int)cnt, ol2);
+                const uint32_t o_zero = (uint32_t)__shfl((int)zero, ol2);
+                const uint32_t o_base = (uint32_t)__shfl((int)base, ol2);
+                const uint32_t o_seq0 = (uint32_t)__shfl((int)seq0, ol2);
+                const uint32_t o_gen = (uint32_t)__shfl((int)s.w, ol2) >> SpecState::GEN;
+                const uint32_t glo = (uint32_t)__shfl((int)(uint32_t)grp, ol2);
+                const uint32_t ghi = (uint32_t)__shfl((int)(uint32_t)(grp >> 32), ol2);
+                if (idle && o_cnt) {
+                    const unsigned long long og = ((unsigned long long)ghi << 32) | glo;
+                    const uint32_t k = (uint32_t)__popcll(og & im & below);  // this lane's rank among the idle
+                    if (k < o_cnt) {
+                        const uint32_t ahead = k + 1u - o_zero;  // full-length samples between base and this start
+                        seed = ahead ? lcg_advance(o_base, guess * ahead) : o_base;
+                        if (COUNT && ahead) n_spec++;
+                        mseq = o_seq0 + k;
+                        mgen = o_gen & 1023u;
                         start = true;
-                        left--;
-                        nif = 1;
-                        s.set(SpecState::HEADH, 1, 0);
                     }
-                    const bool headh = s.headh();
-                    const bool have_tail = headh || s.hasp();  // the tail lane: the owner's or the helper's
-                    if (nif >= 1 && left > 0 && have_tail) {
-                        const bool t_run = headh ? s.srun() : ps.srun();
-                        const bool t_end = headh ? s.send() : ps.send();
-                        const bool t_held = headh ? s.held() : ps.held();
-                        if (nif == 1 && !t_run && !t_end && !t_held) {  // the tail's first sample, guessed
-                            // the head's start: the helper's, or the owner's (just set when it started now)
-                            gst = lcg_advance(headh ? p_start : (start ? seed : sstart), guess);
-                            if (headh) self_guess = true;
-                            else hcmd = CMD_GUESS;
-                            left--;
-                            nif = 2;
-                        } else if (nif == 2 && t_end && !t_held) {  // hold it and go on with the next
-                            if (headh) self_hold = true;
-                            else hcmd = CMD_HOLD;
-                            left--;
-                            nif = 3;
-                        }
-                    }
-                    s.set(SpecState::NIF, 2, nif);
-                }
-                const uint32_t go = (uint32_t)__shfl((int)hcmd, part);
-                const uint32_t gstate = (uint32_t)__shfl((int)gst, part);
-                const uint32_t opix = (uint32_t)__shfl((int)pix, part);
-                if (s.role() == ROLE_HELPER) {
-                    self_guess = go == CMD_GUESS;
-                    self_hold = go == CMD_HOLD;
-                }
-                if (self_guess) {  // from the guessed state (the owner's gst)
-                    if (COUNT) n_spec++;
-                    seed = s.role() == ROLE_HELPER ? gstate : gst;
-                    start = true;
-                }
-                if (self_hold) {  // keep the finished sample, the next one starts from its end state
-                    hL = Lr;
-                    hE = seed;
-                    if (COUNT) {
-                        hc_closest = sc_closest;
-                        hc_shadow = sc_shadow;
-                    }
-                    s.set(SpecState::HELD, 1, 1);
-                    s.set(SpecState::SEND, 1, 0);
-                    start = true;
                 }
                 if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
-                    const uint32_t px = pa.pixel[s.role() == ROLE_HELPER ? opix : pix];
+                    const uint32_t px = pa.pixel[pix];
                     sstart = seed;
                     Lr = V3{0.0f, 0.0f, 0.0f};
                     beta = V3{1.0f, 1.0f, 1.0f};
