@@ -2280,14 +2280,21 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 // group find each other with wave ballots against the owner's group mask; every hand-off is a lane
 // shuffle inside one wave.
 constexpr uint32_t kSpecHelpers = 15;   // helpers per pixel (a group spans at most 16 lanes)
+// How far ahead a pixel may speculate, from its guess record ACC (a saturating count: +1 for a
+// committed sample of the guessed length, halved for any other): samples in flight beyond the head
+__device__ __forceinline__ uint32_t spec_depth(uint32_t acc) {
+    return acc >= 12u ? kSpecHelpers : (acc >= 9u ? 3u : (acc >= 6u ? 1u : 0u));
+}
 enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
 
 struct SpecState {
     uint32_t w = 0;
     // ROLE: free / owner / helper; OL: a helper's owner lane; SRUN: the lane's sample runs; SEND: it
     // ended, (Lr, seed) wait for the commit; NIF (owner): samples in flight; NH (owner): helpers;
-    // GEN (owner): the generation of its samples in flight
-    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NIF = 12, NH = 17, GEN = 22;
+    // GEN (owner): the generation of its samples in flight (a drop clears every sample of the old one
+    // in the same phase, so 4 bits do); ACC (owner): its guess record (spec_depth)
+    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NIF = 12, NH = 17, GEN = 22,
+                              ACC = 26;
     __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
     __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
         const uint32_t m = ((1u << bits) - 1u) << off;
@@ -2301,7 +2308,8 @@ struct SpecState {
     __device__ __forceinline__ bool pend() const { return get(PEND, 1) != 0; }
     __device__ __forceinline__ uint32_t nif() const { return get(NIF, 5); }
     __device__ __forceinline__ uint32_t nh() const { return get(NH, 5); }
-    __device__ __forceinline__ uint32_t gen() const { return get(GEN, 10); }
+    __device__ __forceinline__ uint32_t gen() const { return get(GEN, 4); }
+    __device__ __forceinline__ uint32_t acc() const { return get(ACC, 4); }
 };
 
 template <bool COUNT, bool TAB>
@@ -2452,6 +2460,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 L.y = __shfl(Lr.y, hl);
                 L.z = __shfl(Lr.z, hl);
                 const uint32_t E = (uint32_t)__shfl((int)seed, hl);
+                const uint32_t S0 = (uint32_t)__shfl((int)sstart, hl);
                 uint32_t hcc = 0, hcs = 0;
                 if (COUNT) {
                     hcc = (uint32_t)__shfl((int)sc_closest, hl);
@@ -2468,8 +2477,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     C = E;
                     cseq++;
                     s.set(SpecState::NIF, 5, s.nif() - 1u);
+                    const bool hit = lcg_advance(S0, guess) == E;  // the guessed length was right
+                    s.set(SpecState::ACC, 4, hit ? min(s.acc() + 1u, 15u) : s.acc() >> 1);
                 } else if (drop) {  // every sample in flight: a new generation, rerun from C
-                    s.set(SpecState::GEN, 10, s.gen() + 1u);
+                    s.set(SpecState::GEN, 4, s.gen() + 1u);
+                    s.set(SpecState::ACC, 4, s.acc() >> 1);
                     left += s.nif();
                     nseq = cseq;
                     s.set(SpecState::NIF, 5, 0);
@@ -2517,6 +2529,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     s.set(SpecState::ROLE, 2, ROLE_OWNER);
                     s.set(SpecState::NIF, 5, 0);
                     s.set(SpecState::NH, 5, 0);
+                    s.set(SpecState::ACC, 4, 6);
                     if (COUNT) pc_closest = pc_shadow = 0;
                 }
             }
@@ -2524,7 +2537,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             // per owner per phase; the owners with at least half the wave's most samples left first
             {
                 const bool avail = s.role() == ROLE_FREE && done;
-                const bool want = s.role() == ROLE_OWNER && s.nh() < kSpecHelpers && left > 0;
+                const bool want = s.role() == ROLE_OWNER && s.nh() < spec_depth(s.acc()) && left > 0;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
                 int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
@@ -2563,7 +2576,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const unsigned long long im = __ballot(idle);
                 uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0;
                 if (s.role() == ROLE_OWNER) {
-                    cnt = min((uint32_t)__popcll(grp & im), left);
+                    const uint32_t room = 1u + spec_depth(s.acc()) - min(s.nif(), 1u + spec_depth(s.acc()));
+                    cnt = min(min((uint32_t)__popcll(grp & im), left), room);
                     zero = s.nif() == 0 ? 1u : 0u;
                     base = zero ? C : tstart;
                     seq0 = nseq;
@@ -2578,7 +2592,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const uint32_t o_zero = (uint32_t)__shfl((int)zero, ol2);
                 const uint32_t o_base = (uint32_t)__shfl((int)base, ol2);
                 const uint32_t o_seq0 = (uint32_t)__shfl((int)seq0, ol2);
-                const uint32_t o_gen = (uint32_t)__shfl((int)s.w, ol2) >> SpecState::GEN;
+                const uint32_t o_gen = ((uint32_t)__shfl((int)s.w, ol2) >> SpecState::GEN) & 15u;
                 const uint32_t glo = (uint32_t)__shfl((int)(uint32_t)grp, ol2);
                 const uint32_t ghi = (uint32_t)__shfl((int)(uint32_t)(grp >> 32), ol2);
                 if (idle && o_cnt) {
@@ -2589,7 +2603,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         seed = ahead ? lcg_advance(o_base, guess * ahead) : o_base;
                         if (COUNT && ahead) n_spec++;
                         mseq = o_seq0 + k;
-                        mgen = o_gen & 1023u;
+                        mgen = o_gen & 15u;
                         start = true;
                     }
                 }
