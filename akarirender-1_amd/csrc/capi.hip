@@ -267,6 +267,7 @@ struct akr_hip_ctx {
     // slower, profiles/r19_spec_ab.log)
     int path_spec = 2;
     int64_t path_spec_pixels = 1200000;
+    int path_spec_fetch = 3;  // k_path_spec's ordered fetch: FETCH_STRIDE (3); -1 = the path_order_pair rule
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
@@ -1027,6 +1028,9 @@ struct akr_hip_ctx {
                     const bool pair = path_order_pair == 3 ||
                                       (kind != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000)));
                     pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
+                    // k_path_spec: every wave takes pixels from the whole cost order (FETCH_STRIDE), so
+                    // each has cheap pixels whose lanes turn helpers early (option path_spec_fetch)
+                    if (kind == PATH_SPEC && path_spec_fetch >= 0) pa.order_mode = (uint32_t)path_spec_fetch;
                     pa.prio = (uint32_t)path_prio;
                 }
                 timed("path", ms, [&] { launch_path(count, kind, tab, pa, grid, ms); });
@@ -1367,6 +1371,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec") {
             if (value < 0 || value > 2) throw std::runtime_error("path_spec must be 0, 1 or 2");
             ctx->path_spec = (int)value;
+        } else if (k == "path_spec_fetch") {
+            if (value < -1 || value > 3) throw std::runtime_error("path_spec_fetch must be in [-1, 3]");
+            ctx->path_spec_fetch = (int)value;
         } else if (k == "path_spec_pixels") {
             if (value < 0) throw std::runtime_error("path_spec_pixels must be >= 0");
             ctx->path_spec_pixels = value;

@@ -1585,12 +1585,21 @@ __device__ __forceinline__ void path_unpark(uint32_t (*s_park)[kTraceBlock], uin
 // take the long pixels' shadow rays).  `order` (optional) maps the position to the
 // slot.  With `prio`, a wave whose fetch lies in the first `prio` / 256 of its shard (the costliest
 // pixels of a cost order) raises its issue priority, else lowers it.
-enum : uint32_t { FETCH_LINEAR = 0, FETCH_SCRAMBLE = 1, FETCH_PAIR = 2 };
+enum : uint32_t { FETCH_LINEAR = 0, FETCH_SCRAMBLE = 1, FETCH_PAIR = 2, FETCH_STRIDE = 3 };
 struct PixelFetch {
     uint32_t shard, s_lo, s_hi;
     int shards_left;
     bool drained;
+    uint32_t stride = 0;  // FETCH_STRIDE: the shard's step (coprime with its length), 0 = not computed
 };
+__device__ __forceinline__ uint32_t gcd_u32(uint32_t x, uint32_t y) {
+    while (y) {
+        const uint32_t t = x % y;
+        x = y;
+        y = t;
+    }
+    return x;
+}
 __device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t *work, uint32_t mode,
                                              const uint32_t *order, uint32_t prio, bool &need, bool &done,
                                              uint32_t &pix) {
@@ -1617,6 +1626,14 @@ __device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t
                 uint32_t pos = my;
                 if (mode == FETCH_SCRAMBLE) pos = (uint32_t)(((uint64_t)my * 2147483647ull) % len);
                 else if (mode == FETCH_PAIR) pos = (my & 1u) ? len - 1u - (my >> 1) : (my >> 1);
+                else if (mode == FETCH_STRIDE) {  // consecutive fetches len/64 apart: every wave spans the cost order
+                    if (f.stride == 0) {
+                        uint32_t st = max(1u, len / 64u) | 1u;
+                        while (gcd_u32(st, len) != 1u) st += 2u;
+                        f.stride = st;
+                    }
+                    pos = (uint32_t)(((uint64_t)my * f.stride) % len);
+                }
                 const uint32_t at = f.s_lo + pos;
                 pix = order ? order[at] : at;
                 need = false;
@@ -1631,6 +1648,7 @@ __device__ __forceinline__ void fetch_pixels(PixelFetch &f, uint32_t n, uint32_t
                 f.shard = (f.shard + 1) % kWorkShards;
                 f.s_lo = shard_begin(n, f.shard);
                 f.s_hi = shard_begin(n, f.shard + 1);
+                f.stride = 0;
                 const uint32_t taken = __builtin_amdgcn_readfirstlane(
                     __hip_atomic_load(work + f.shard * kWorkStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 if (taken < f.s_hi - f.s_lo) break;
@@ -2280,11 +2298,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 // group find each other with wave ballots against the owner's group mask; every hand-off is a lane
 // shuffle inside one wave.
 constexpr uint32_t kSpecHelpers = 15;   // helpers per pixel (a group spans at most 16 lanes)
-// How far ahead a pixel may speculate, from its guess record ACC (a saturating count: +1 for a
-// committed sample of the guessed length, halved for any other): samples in flight beyond the head
-__device__ __forceinline__ uint32_t spec_depth(uint32_t acc) {
-    return acc >= 12u ? kSpecHelpers : (acc >= 9u ? 3u : (acc >= 6u ? 1u : 0u));
-}
+
 enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
 
 struct SpecState {
@@ -2292,9 +2306,8 @@ struct SpecState {
     // ROLE: free / owner / helper; OL: a helper's owner lane; SRUN: the lane's sample runs; SEND: it
     // ended, (Lr, seed) wait for the commit; NIF (owner): samples in flight; NH (owner): helpers;
     // GEN (owner): the generation of its samples in flight (a drop clears every sample of the old one
-    // in the same phase, so 4 bits do); ACC (owner): its guess record (spec_depth)
-    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NIF = 12, NH = 17, GEN = 22,
-                              ACC = 26;
+    // in the same phase, so 4 bits do)
+    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NIF = 12, NH = 17, GEN = 22;
     __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
     __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
         const uint32_t m = ((1u << bits) - 1u) << off;
@@ -2309,7 +2322,6 @@ struct SpecState {
     __device__ __forceinline__ uint32_t nif() const { return get(NIF, 5); }
     __device__ __forceinline__ uint32_t nh() const { return get(NH, 5); }
     __device__ __forceinline__ uint32_t gen() const { return get(GEN, 4); }
-    __device__ __forceinline__ uint32_t acc() const { return get(ACC, 4); }
 };
 
 template <bool COUNT, bool TAB>
@@ -2460,7 +2472,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 L.y = __shfl(Lr.y, hl);
                 L.z = __shfl(Lr.z, hl);
                 const uint32_t E = (uint32_t)__shfl((int)seed, hl);
-                const uint32_t S0 = (uint32_t)__shfl((int)sstart, hl);
                 uint32_t hcc = 0, hcs = 0;
                 if (COUNT) {
                     hcc = (uint32_t)__shfl((int)sc_closest, hl);
@@ -2477,11 +2488,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     C = E;
                     cseq++;
                     s.set(SpecState::NIF, 5, s.nif() - 1u);
-                    const bool hit = lcg_advance(S0, guess) == E;  // the guessed length was right
-                    s.set(SpecState::ACC, 4, hit ? min(s.acc() + 1u, 15u) : s.acc() >> 1);
                 } else if (drop) {  // every sample in flight: a new generation, rerun from C
                     s.set(SpecState::GEN, 4, s.gen() + 1u);
-                    s.set(SpecState::ACC, 4, s.acc() >> 1);
                     left += s.nif();
                     nseq = cseq;
                     s.set(SpecState::NIF, 5, 0);
@@ -2529,7 +2537,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     s.set(SpecState::ROLE, 2, ROLE_OWNER);
                     s.set(SpecState::NIF, 5, 0);
                     s.set(SpecState::NH, 5, 0);
-                    s.set(SpecState::ACC, 4, 6);
                     if (COUNT) pc_closest = pc_shadow = 0;
                 }
             }
@@ -2537,7 +2544,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             // per owner per phase; the owners with at least half the wave's most samples left first
             {
                 const bool avail = s.role() == ROLE_FREE && done;
-                const bool want = s.role() == ROLE_OWNER && s.nh() < spec_depth(s.acc()) && left > 0;
+                const bool want = s.role() == ROLE_OWNER && s.nh() < kSpecHelpers && left > 0;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
                 int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
@@ -2576,8 +2583,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const unsigned long long im = __ballot(idle);
                 uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0;
                 if (s.role() == ROLE_OWNER) {
-                    const uint32_t room = 1u + spec_depth(s.acc()) - min(s.nif(), 1u + spec_depth(s.acc()));
-                    cnt = min(min((uint32_t)__popcll(grp & im), left), room);
+                    cnt = min((uint32_t)__popcll(grp & im), left);
                     zero = s.nif() == 0 ? 1u : 0u;
                     base = zero ? C : tstart;
                     seq0 = nseq;
