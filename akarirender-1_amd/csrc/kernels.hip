@@ -2544,7 +2544,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             // per owner per phase; the owners with at least half the wave's most samples left first
             {
                 const bool avail = s.role() == ROLE_FREE && done;
-                const bool want = s.role() == ROLE_OWNER && s.nh() < kSpecHelpers && left > 0;
+                const bool want = s.role() == ROLE_OWNER && s.nh() < min(kSpecHelpers, pa.spec_depth) && left > 0;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
                 int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
@@ -2583,7 +2583,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const unsigned long long im = __ballot(idle);
                 uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0;
                 if (s.role() == ROLE_OWNER) {
-                    cnt = min((uint32_t)__popcll(grp & im), left);
+                    // at most spec_depth samples in flight beyond the head (option path_spec_depth)
+                    const uint32_t cap = 1u + pa.spec_depth, nif = s.nif();
+                    cnt = min(min((uint32_t)__popcll(grp & im), left), cap > nif ? cap - nif : 0u);
                     zero = s.nif() == 0 ? 1u : 0u;
                     base = zero ? C : tstart;
                     seq0 = nseq;
