@@ -268,7 +268,8 @@ struct akr_hip_ctx {
     int path_spec = 2;
     int64_t path_spec_pixels = 1200000;
     int path_spec_fetch = 3;
-    int path_spec_depth = 15;  // option "path_spec_depth": k_path_spec's samples in flight beyond a pixel's head (1-15)  // k_path_spec's ordered fetch: FETCH_STRIDE (3); -1 = the path_order_pair rule
+    int path_spec_depth = 4;   // option "path_spec_depth": k_path_spec's main-line samples in flight beyond a pixel's head (1-14)
+    bool path_spec_alt = true; // option "path_spec_alt": k_path_spec also runs the one-bounce alternative  // k_path_spec's ordered fetch: FETCH_STRIDE (3); -1 = the path_order_pair rule
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
@@ -997,6 +998,7 @@ struct akr_hip_ctx {
                 pa.fault_test = fault_test ? 1u : 0u;
                 pa.probe_clock = probe_clock ? 1u : 0u;
                 pa.spec_depth = (uint32_t)path_spec_depth;
+                pa.spec_alt = path_spec_alt ? 1u : 0u;
                 const bool defer = p.max_depth <= 8 &&
                                    (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels &&
                                                         (int64_t)n_tris() >= path_defer_min_tris));
@@ -1373,8 +1375,10 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec") {
             if (value < 0 || value > 2) throw std::runtime_error("path_spec must be 0, 1 or 2");
             ctx->path_spec = (int)value;
+        } else if (k == "path_spec_alt") {
+            ctx->path_spec_alt = value != 0;
         } else if (k == "path_spec_depth") {
-            if (value < 1 || value > 15) throw std::runtime_error("path_spec_depth must be in [1, 15]");
+            if (value < 1 || value > 14) throw std::runtime_error("path_spec_depth must be in [1, 14]");
             ctx->path_spec_depth = (int)value;
         } else if (k == "path_spec_fetch") {
             if (value < -1 || value > 3) throw std::runtime_error("path_spec_fetch must be in [-1, 3]");

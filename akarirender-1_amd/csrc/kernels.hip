@@ -2291,23 +2291,28 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 // it is the head, otherwise from the guessed state lcg_advance(start(previous sample), g) with
 // g = 4 + 6 max_depth (a full-length path: on the C3 soup the costliest pixels' samples are full
 // length 91-100 % of the time, tools/sample_lengths.py), so the k-th sample ahead is k guesses deep.
+// Besides that main line, one helper may run an alternative for the sample after the head, from
+// lcg_advance(C, 4 + 6) (a one-bounce head: the soup's other common length, 34 % of its samples).
 // The owner commits in order: a finished head whose start is C is added to the film
-// (Tile::add_sample, core/film.h:66-70) and C becomes its end state; a head whose start is not C
-// was guessed wrong, and every sample in flight is dropped (a new generation) and rerun.  So the
+// (Tile::add_sample, core/film.h:66-70) and C becomes its end state.  Of the candidates for the next
+// head (the main-line sample and the alternative) the one that starts from C is kept: when it is the
+// alternative, the main line from there on is dropped (a new generation, in which the alternative
+// was started); when neither does, every sample in flight is dropped (two generations on) and rerun.  So the
 // film sums and the final sampler state are the sequential loop's, bit for bit.  The lanes of a
 // group find each other with wave ballots against the owner's group mask; every hand-off is a lane
 // shuffle inside one wave.
 constexpr uint32_t kSpecHelpers = 15;   // helpers per pixel (a group spans at most 16 lanes)
-
 enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
 
 struct SpecState {
     uint32_t w = 0;
     // ROLE: free / owner / helper; OL: a helper's owner lane; SRUN: the lane's sample runs; SEND: it
-    // ended, (Lr, seed) wait for the commit; NIF (owner): samples in flight; NH (owner): helpers;
-    // GEN (owner): the generation of its samples in flight (a drop clears every sample of the old one
-    // in the same phase, so 4 bits do)
-    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NIF = 12, NH = 17, GEN = 22;
+    // ended, (Lr, seed) wait for the commit; ALT (owner): an alternative sample is in flight; MALT
+    // (any lane): its sample was started as that alternative; NH (owner): helpers; GEN (owner): the
+    // generation of the main line in flight (the alternative is started in GEN + 1; a drop clears
+    // every sample of an old generation in the same phase, so 4 bits do)
+    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, ALT = 12, MALT = 13, NH = 17,
+                              GEN = 22;
     __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
     __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
         const uint32_t m = ((1u << bits) - 1u) << off;
@@ -2319,7 +2324,8 @@ struct SpecState {
     __device__ __forceinline__ bool send() const { return get(SEND, 1) != 0; }
     __device__ __forceinline__ bool any() const { return get(ANY, 1) != 0; }
     __device__ __forceinline__ bool pend() const { return get(PEND, 1) != 0; }
-    __device__ __forceinline__ uint32_t nif() const { return get(NIF, 5); }
+    __device__ __forceinline__ bool alt() const { return get(ALT, 1) != 0; }
+    __device__ __forceinline__ bool malt() const { return get(MALT, 1) != 0; }
     __device__ __forceinline__ uint32_t nh() const { return get(NH, 5); }
     __device__ __forceinline__ uint32_t gen() const { return get(GEN, 4); }
 };
@@ -2339,6 +2345,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const uint32_t n = pa.n_pix;
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
     const uint32_t guess = 4u + 6u * (uint32_t)pa.max_depth;  // draws of a full-length sample
+    const uint32_t galt = 4u + 6u;                             // draws of a one-bounce sample (the alternative)
+    const uint32_t spp = pa.spp;
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
     PathCount c;
@@ -2346,10 +2354,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     f.s_lo = shard_begin(n, f.shard);
     f.s_hi = shard_begin(n, f.shard + 1);
 
-    // owner: the samples not yet started, the committed state, the start of the last started sample,
-    // the next sample to commit / to start, its group's lanes; every group lane: the pixel, and the
-    // sample it runs (its state, start, number and generation)
-    uint32_t pix = 0, left = 0, C = 0, tstart = 0, cseq = 0, nseq = 0;
+    // owner: the committed state, the start of the last main-line sample started, the next sample to
+    // commit / to start on the main line (nseq - cseq in flight, spp - nseq not started), its group's
+    // lanes; every group lane: the pixel, and the sample it runs (its state, start, number, generation)
+    uint32_t pix = 0, C = 0, tstart = 0, cseq = 0, nseq = 0;
     unsigned long long grp = 0;
     uint32_t seed = 0, sstart = 0, mseq = 0, mgen = 0;
     int depth = 0;
@@ -2453,56 +2461,71 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const uint32_t o_C = (uint32_t)__shfl((int)C, ol);
                 SpecState os;
                 os.w = (uint32_t)__shfl((int)s.w, ol);
-                const bool mine = in_grp && (s.srun() || s.send()) && mgen == os.gen();
-                const bool head = mine && mseq == o_cseq;
-                const bool bad = head && sstart != o_C;      // a wrong guess reached the head
-                const bool ready = head && !bad && s.send();  // a finished head: commit it
-                const unsigned long long badm = __ballot(bad), rdm = __ballot(ready);
-                if ((badm | rdm) == 0) break;
-                int hl = (int)lane;
-                bool commit = false, drop = false;
-                if (s.role() == ROLE_OWNER) {
-                    drop = (grp & badm) != 0;
-                    const unsigned long long m = grp & rdm;
-                    commit = !drop && m != 0;
-                    if (commit) hl = __ffsll((long long)m) - 1;
-                }
+                const uint32_t g0 = os.gen();
+                const bool mine = in_grp && (s.srun() || s.send()) &&
+                                  (mgen == g0 || (s.malt() && mgen == ((g0 + 1u) & 15u)));
+                const bool cand = mine && mseq == o_cseq;  // a candidate for the head
+                const bool valid = cand && sstart == o_C;   // ... that starts from C
+                const unsigned long long cbm = __ballot(cand), vm = __ballot(valid);
+                if (cbm == 0) break;
+                // owners: their valid candidate's lane (every lane shuffles from it, or from itself)
+                const bool act = s.role() == ROLE_OWNER && (grp & cbm) != 0;
+                const unsigned long long v = grp & vm;
+                const int hl = act && v ? __ffsll((long long)v) - 1 : (int)lane;
                 V3 L;
                 L.x = __shfl(Lr.x, hl);
                 L.y = __shfl(Lr.y, hl);
                 L.z = __shfl(Lr.z, hl);
                 const uint32_t E = (uint32_t)__shfl((int)seed, hl);
+                const uint32_t hflags = (uint32_t)__shfl((int)((s.send() ? 1u : 0u) | (mgen == g0 ? 0u : 2u)), hl);
                 uint32_t hcc = 0, hcs = 0;
                 if (COUNT) {
                     hcc = (uint32_t)__shfl((int)sc_closest, hl);
                     hcs = (uint32_t)__shfl((int)sc_shadow, hl);
                 }
-                if (commit) {
-                    float4 fm = pa.film[pix];  // the film sums live in the (zeroed) film slot
-                    splat_one(fm, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
-                    pa.film[pix] = fm;
-                    if (COUNT) {
-                        pc_closest += hcc;
-                        pc_shadow += hcs;
+                bool changed = false;
+                if (act) {
+                    if (v == 0) {  // no candidate starts from C: drop the main line and the alternative
+                        s.set(SpecState::GEN, 4, g0 + 2u);
+                        s.set(SpecState::ALT, 1, 0);
+                        nseq = cseq;
+                        changed = true;
+                    } else {
+                        if (hflags & 2u) {  // the alternative starts from C: it becomes the main line
+                            s.set(SpecState::GEN, 4, g0 + 1u);
+                            s.set(SpecState::ALT, 1, 0);
+                            nseq = cseq + 1u;
+                            tstart = o_C;
+                            changed = true;
+                        } else if (s.alt() && (grp & cbm & ~vm)) {  // the main line holds: the alternative goes
+                            s.set(SpecState::ALT, 1, 0);
+                            changed = true;
+                        }
+                        if (hflags & 1u) {  // the head ended: Tile::add_sample, C = its end state
+                            float4 fm = pa.film[pix];  // the film sums live in the (zeroed) film slot
+                            splat_one(fm, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
+                            pa.film[pix] = fm;
+                            if (COUNT) {
+                                pc_closest += hcc;
+                                pc_shadow += hcs;
+                            }
+                            C = E;
+                            cseq++;
+                            changed = true;
+                        }
                     }
-                    C = E;
-                    cseq++;
-                    s.set(SpecState::NIF, 5, s.nif() - 1u);
-                } else if (drop) {  // every sample in flight: a new generation, rerun from C
-                    s.set(SpecState::GEN, 4, s.gen() + 1u);
-                    left += s.nif();
-                    nseq = cseq;
-                    s.set(SpecState::NIF, 5, 0);
                 }
+                if (__ballot(changed) == 0) break;
             }
             // each group lane: its sample committed or dropped -> idle; a pixel that is done frees
             // its group
             {
-                if (s.role() == ROLE_OWNER && s.nif() == 0 && left == 0) {  // the pixel is done
+                if (s.role() == ROLE_OWNER && cseq == spp) {  // the pixel is done
                     if (pa.probe)
                         pa.probe[pix] = make_uint4(C, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u, probe_flags<COUNT>(pa));
                     s.set(SpecState::ROLE, 2, ROLE_FREE);
                     s.set(SpecState::NH, 5, 0);
+                    s.set(SpecState::ALT, 1, 0);
                     grp = 0;
                 }
                 SpecState os;
@@ -2511,14 +2534,20 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 const uint32_t o_pix = (uint32_t)__shfl((int)pix, ol);
                 if (s.role() == ROLE_HELPER && (os.role() != ROLE_OWNER || o_pix != pix))
                     s.set(SpecState::ROLE, 2, ROLE_FREE);  // its pixel is done (its lane may own another)
+                const uint32_t g0 = os.gen();
+                if (s.malt() && mgen == g0) s.set(SpecState::MALT, 1, 0);  // an alternative that became the main line
+                const bool is_main = mgen == g0;
+                const bool is_alt = s.malt() && mgen == ((g0 + 1u) & 15u);
                 const bool had = s.srun() || s.send();
-                const bool gone = had && (s.role() == ROLE_FREE || mgen != os.gen() || mseq < o_cseq);
+                const bool gone = had && (s.role() == ROLE_FREE || (!is_main && !is_alt) ||
+                                          (is_main && mseq < o_cseq) || (is_alt && (!os.alt() || mseq < o_cseq)));
                 if (gone) {
-                    const bool committed = s.role() != ROLE_FREE && mgen == os.gen() && mseq < o_cseq;
+                    const bool committed = s.role() != ROLE_FREE && is_main && mseq < o_cseq;
                     if (COUNT && !committed) n_abort++;
                     s.set(SpecState::SRUN, 1, 0);
                     s.set(SpecState::SEND, 1, 0);
                     s.set(SpecState::PEND, 1, 0);
+                    s.set(SpecState::MALT, 1, 0);
                     fresh = false;  // a dropped sample's ray goes with it
                     busy = false;
                 }
@@ -2530,12 +2559,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 fetch_pixels(f, n, pa.work, pa.order ? pa.order_mode : FETCH_LINEAR, pa.order, pa.prio, need, done, pix);
                 if (asked && !need) {
                     const uint32_t px = pa.pixel[pix];
-                    left = pa.spp;
                     C = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
                     cseq = nseq = 0;
                     grp = 1ull << lane;
                     s.set(SpecState::ROLE, 2, ROLE_OWNER);
-                    s.set(SpecState::NIF, 5, 0);
+                    s.set(SpecState::ALT, 1, 0);
                     s.set(SpecState::NH, 5, 0);
                     if (COUNT) pc_closest = pc_shadow = 0;
                 }
@@ -2544,7 +2572,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             // per owner per phase; the owners with at least half the wave's most samples left first
             {
                 const bool avail = s.role() == ROLE_FREE && done;
-                const bool want = s.role() == ROLE_OWNER && s.nh() < min(kSpecHelpers, pa.spec_depth) && left > 0;
+                const uint32_t left = spp - nseq;  // main-line samples not started
+                const bool want = s.role() == ROLE_OWNER && s.nh() < min(kSpecHelpers, pa.spec_depth + 1u) && left > 0;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
                 int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
@@ -2575,35 +2604,42 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     pix = np;
                 }
             }
-            // 5. starts: the idle lanes of a group take the next samples in lane order, the first from C
-            // when nothing is in flight, every other from the guessed state one full-length sample on
+            // 5. starts: the idle lanes of a group take the next main-line samples in lane order (the
+            // first from C when nothing is in flight, every other from the guessed state one full-length
+            // sample on; at most spec_depth beyond the head), then one more may take the alternative
             {
                 const int ol2 = s.role() == ROLE_HELPER ? (int)s.ol() : (int)lane;
                 const bool idle = s.role() != ROLE_FREE && !s.srun() && !s.send();
                 const unsigned long long im = __ballot(idle);
-                uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0;
+                uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0, ago = 0, astart = 0;
                 if (s.role() == ROLE_OWNER) {
-                    // at most spec_depth samples in flight beyond the head (option path_spec_depth)
-                    const uint32_t cap = 1u + pa.spec_depth, nif = s.nif();
-                    cnt = min(min((uint32_t)__popcll(grp & im), left), cap > nif ? cap - nif : 0u);
-                    zero = s.nif() == 0 ? 1u : 0u;
+                    const uint32_t nfree = (uint32_t)__popcll(grp & im);
+                    const uint32_t inflight = nseq - cseq, cap = 1u + pa.spec_depth;
+                    cnt = min(min(nfree, spp - nseq), cap > inflight ? cap - inflight : 0u);
+                    zero = inflight == 0 ? 1u : 0u;
                     base = zero ? C : tstart;
                     seq0 = nseq;
                     if (cnt) {
                         tstart = lcg_advance(base, guess * (cnt - zero));  // the last new sample's start
                         nseq += cnt;
-                        left -= cnt;
-                        s.set(SpecState::NIF, 5, s.nif() + cnt);
+                    }
+                    if (pa.spec_alt && !s.alt() && nfree > cnt && nseq > cseq && cseq + 1u < spp && galt != guess) {
+                        ago = 1;
+                        astart = lcg_advance(C, galt);  // the sample after a one-bounce head
+                        s.set(SpecState::ALT, 1, 1);
                     }
                 }
                 const uint32_t o_cnt = (uint32_t)__shfl((int)cnt, ol2);
                 const uint32_t o_zero = (uint32_t)__shfl((int)zero, ol2);
                 const uint32_t o_base = (uint32_t)__shfl((int)base, ol2);
                 const uint32_t o_seq0 = (uint32_t)__shfl((int)seq0, ol2);
+                const uint32_t o_ago = (uint32_t)__shfl((int)ago, ol2);
+                const uint32_t o_astart = (uint32_t)__shfl((int)astart, ol2);
+                const uint32_t o_cseq = (uint32_t)__shfl((int)cseq, ol2);
                 const uint32_t o_gen = ((uint32_t)__shfl((int)s.w, ol2) >> SpecState::GEN) & 15u;
                 const uint32_t glo = (uint32_t)__shfl((int)(uint32_t)grp, ol2);
                 const uint32_t ghi = (uint32_t)__shfl((int)(uint32_t)(grp >> 32), ol2);
-                if (idle && o_cnt) {
+                if (idle && (o_cnt || o_ago)) {
                     const unsigned long long og = ((unsigned long long)ghi << 32) | glo;
                     const uint32_t k = (uint32_t)__popcll(og & im & below);  // this lane's rank among the idle
                     if (k < o_cnt) {
@@ -2611,7 +2647,14 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         seed = ahead ? lcg_advance(o_base, guess * ahead) : o_base;
                         if (COUNT && ahead) n_spec++;
                         mseq = o_seq0 + k;
-                        mgen = o_gen & 15u;
+                        mgen = o_gen;
+                        start = true;
+                    } else if (o_ago && k == o_cnt) {  // the alternative, one generation on
+                        seed = o_astart;
+                        if (COUNT) n_spec++;
+                        mseq = o_cseq + 1u;
+                        mgen = (o_gen + 1u) & 15u;
+                        s.set(SpecState::MALT, 1, 1);
                         start = true;
                     }
                 }
