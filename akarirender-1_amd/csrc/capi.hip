@@ -269,7 +269,7 @@ struct akr_hip_ctx {
     int64_t path_spec_pixels = 1200000;
     int path_spec_fetch = 3;
     int path_spec_depth = 4;   // option "path_spec_depth": k_path_spec's main-line samples in flight beyond a pixel's head (1-14)
-    bool path_spec_alt = true; // option "path_spec_alt": k_path_spec also runs the one-bounce alternative  // k_path_spec's ordered fetch: FETCH_STRIDE (3); -1 = the path_order_pair rule
+    bool path_spec_alt = false;  // option "path_spec_alt": k_path_spec also runs the one-bounce alternative (measured: no gain)  // k_path_spec's ordered fetch: FETCH_STRIDE (3); -1 = the path_order_pair rule
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
