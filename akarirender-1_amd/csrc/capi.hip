@@ -267,9 +267,12 @@ struct akr_hip_ctx {
     // slower, profiles/r19_spec_ab.log)
     int path_spec = 2;
     int64_t path_spec_pixels = 1200000;
-    int path_spec_fetch = 3;
-    int path_spec_depth = 4;   // option "path_spec_depth": k_path_spec's main-line samples in flight beyond a pixel's head (1-14)
-    bool path_spec_alt = false;  // option "path_spec_alt": k_path_spec also runs the one-bounce alternative (measured: no gain)  // k_path_spec's ordered fetch: FETCH_STRIDE (3); -1 = the path_order_pair rule
+    // (the 8-way share and the whole frame re-measured with the lane groups: 0.82 / 4.85 ms against
+    // 0.86 / 4.61 ms for k_path_defer / k_path, profiles/r19_spec_*.log)
+    int path_spec_fetch = 3;   // option "path_spec_fetch": k_path_spec's ordered fetch, FETCH_STRIDE (3); -1 = the path_order_pair rule
+    int path_spec_depth = 4;   // option "path_spec_depth": main-line samples in flight beyond a pixel's head (1-14;
+                               // 2, 4, 8, 15 measured alike on the 8-way share, 1 slower, profiles/r19_spec_depth.log)
+    bool path_spec_alt = false;  // option "path_spec_alt": also the one-bounce alternative (measured: no gain)
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
