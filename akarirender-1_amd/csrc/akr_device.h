@@ -304,8 +304,8 @@ struct PathArgs {
                                    // build adds the pixel's closest-hit and shadow rays
     uint32_t *fault;               // mapped host word: set when a wave stops on the hang guard (k_path_defer)
     uint32_t fault_test;           // test only: k_path_defer raises `fault` once at the end of the launch
-    uint32_t spec_depth;           // k_path_spec: main-line samples in flight beyond a pixel's head
-    uint32_t spec_alt;             // k_path_spec: also run the one-bounce alternative of the sample after the head
+    uint32_t spec_depth;           // k_path_spec: levels of the speculation tree (samples beyond the head)
+    uint32_t spec_alt;             // k_path_spec: the tree's one-bounce branches too
     uint32_t probe_clock;          // diagnostic (counting build, option "pixel_probe" 2): the probe's flags
                                    // carry the pixel's completion time, (wall clock >> 4) << 8 | flags
 };

@@ -270,9 +270,10 @@ struct akr_hip_ctx {
     // (the 8-way share and the whole frame re-measured with the lane groups: 0.82 / 4.85 ms against
     // 0.86 / 4.61 ms for k_path_defer / k_path, profiles/r19_spec_*.log)
     int path_spec_fetch = 3;   // option "path_spec_fetch": k_path_spec's ordered fetch, FETCH_STRIDE (3); -1 = the path_order_pair rule
-    int path_spec_depth = 4;   // option "path_spec_depth": main-line samples in flight beyond a pixel's head (1-14;
-                               // 2, 4, 8, 15 measured alike on the 8-way share, 1 slower, profiles/r19_spec_depth.log)
-    bool path_spec_alt = false;  // option "path_spec_alt": also the one-bounce alternative (measured: no gain)
+    int path_spec_depth = 3;   // option "path_spec_depth": samples in flight beyond a pixel's head (1-3, the
+                               // speculation tree's levels; the r19 main line measured 2, 4, 8, 15 alike, 1 slower,
+                               // profiles/r19_spec_depth.log)
+    bool path_spec_alt = false;  // option "path_spec_alt": the tree's one-bounce branches too (measured slower)
     int64_t path_defer_pixels = 600000;
     // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
     // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
@@ -1381,7 +1382,7 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec_alt") {
             ctx->path_spec_alt = value != 0;
         } else if (k == "path_spec_depth") {
-            if (value < 1 || value > 14) throw std::runtime_error("path_spec_depth must be in [1, 14]");
+            if (value < 1 || value > 3) throw std::runtime_error("path_spec_depth must be in [1, 3]");
             ctx->path_spec_depth = (int)value;
         } else if (k == "path_spec_fetch") {
             if (value < -1 || value > 3) throw std::runtime_error("path_spec_fetch must be in [-1, 3]");

@@ -2285,34 +2285,35 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 // pixels of their wave by running their later samples speculatively.  A pixel's samples are
 // sequential only through its sampler state (cpu/integrator.cpp:124-134): sample s + 1 starts where
 // sample s stopped drawing, 4 + 6 k draws later for k scattering events (pathtracer.h:96-164).
-// A pixel is run by a group of lanes: its owner (the pixel, its film slot, the committed state C,
-// the samples not yet started) and up to kSpecHelpers helpers.  The samples in flight are numbered
-// (seq); the one numbered like the next commit (cseq) is the head.  A new sample starts from C when
-// it is the head, otherwise from the guessed state lcg_advance(start(previous sample), g) with
-// g = 4 + 6 max_depth (a full-length path: on the C3 soup the costliest pixels' samples are full
-// length 91-100 % of the time, tools/sample_lengths.py), so the k-th sample ahead is k guesses deep.
-// Besides that main line, one helper may run an alternative for the sample after the head, from
-// lcg_advance(C, 4 + 6) (a one-bounce head: the soup's other common length, 34 % of its samples).
-// The owner commits in order: a finished head whose start is C is added to the film
-// (Tile::add_sample, core/film.h:66-70) and C becomes its end state.  Of the candidates for the next
-// head (the main-line sample and the alternative) the one that starts from C is kept: when it is the
-// alternative, the main line from there on is dropped (a new generation, in which the alternative
-// was started); when neither does, every sample in flight is dropped (two generations on) and rerun.  So the
-// film sums and the final sampler state are the sequential loop's, bit for bit.  The lanes of a
-// group find each other with wave ballots against the owner's group mask; every hand-off is a lane
-// shuffle inside one wave.
-constexpr uint32_t kSpecHelpers = 15;   // helpers per pixel (a group spans at most 16 lanes)
+// A pixel is run by a group of lanes: its owner (the pixel, its film slot, the committed state C and
+// count) and up to kSpecHelpers helpers.  Each lane of a group runs one node of a speculation tree:
+// node 0 is the head, the next sample to commit, started from C; a node on level l (1..3) is the
+// sample l places after the head, started from lcg_advance(C, the draws of the l samples before it),
+// each of which it assumes to be full length (4 + 6 max_depth) or one bounce long (4 + 6) — the two
+// common lengths of the C3 soup's samples (46 % and 34 %, tools/sample_lengths.py); its code holds
+// those l choices.  Idle lanes take the free nodes in order of expected use.  When the head ends the
+// owner commits it (Tile::add_sample, core/film.h:66-70), C becomes its end state, and its length
+// picks the branch: the nodes whose first choice it is move up a level (the level-1 one becomes the
+// head: it did start from the new C), the others are dropped; a length that is neither drops every
+// node.  So a committed sample is always the one that starts from the committed state, and the film
+// sums and the final sampler state are the sequential loop's, bit for bit.  The lanes of a group find
+// each other with wave ballots against the owner's group mask; every hand-off is a lane shuffle.
+constexpr uint32_t kSpecNodes = 15;     // the head and 2 + 4 + 8 nodes on levels 1-3 (a group spans at most 15 lanes)
+// nodes in order of expected use (a sample full length with p = 0.6, one bounce with q = 0.35):
+// 0, 1, 3, 2, 7, 4, 5, 8, 9, 11, 6, 12, 13, 10, 14, one per nibble
+constexpr unsigned long long kSpecNodeOrder = 0xEADC6B985472310ull;
 enum : uint32_t { ROLE_FREE = 0, ROLE_OWNER = 1, ROLE_HELPER = 2 };
+enum : uint32_t { BR_FULL = 0, BR_ONE = 1, BR_NONE = 2, BR_NOCOMMIT = 3 };  // the head's branch, broadcast
+
+__device__ __forceinline__ uint32_t node_lvl(uint32_t nd) { return 31u - __clz(nd + 1u); }
+__device__ __forceinline__ uint32_t node_code(uint32_t nd) { return nd + 1u - (1u << node_lvl(nd)); }
 
 struct SpecState {
     uint32_t w = 0;
     // ROLE: free / owner / helper; OL: a helper's owner lane; SRUN: the lane's sample runs; SEND: it
-    // ended, (Lr, seed) wait for the commit; ALT (owner): an alternative sample is in flight; MALT
-    // (any lane): its sample was started as that alternative; NH (owner): helpers; GEN (owner): the
-    // generation of the main line in flight (the alternative is started in GEN + 1; a drop clears
-    // every sample of an old generation in the same phase, so 4 bits do)
-    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, ALT = 12, MALT = 13, NH = 17,
-                              GEN = 22;
+    // ended, (Lr, seed) wait for the commit; NODE: the lane's node in its group's tree; NH (owner):
+    // helpers
+    static constexpr uint32_t ROLE = 0, OL = 2, SRUN = 8, SEND = 9, ANY = 10, PEND = 11, NODE = 12, NH = 17;
     __device__ __forceinline__ uint32_t get(uint32_t off, uint32_t bits) const { return (w >> off) & ((1u << bits) - 1u); }
     __device__ __forceinline__ void set(uint32_t off, uint32_t bits, uint32_t v) {
         const uint32_t m = ((1u << bits) - 1u) << off;
@@ -2324,10 +2325,8 @@ struct SpecState {
     __device__ __forceinline__ bool send() const { return get(SEND, 1) != 0; }
     __device__ __forceinline__ bool any() const { return get(ANY, 1) != 0; }
     __device__ __forceinline__ bool pend() const { return get(PEND, 1) != 0; }
-    __device__ __forceinline__ bool alt() const { return get(ALT, 1) != 0; }
-    __device__ __forceinline__ bool malt() const { return get(MALT, 1) != 0; }
+    __device__ __forceinline__ uint32_t node() const { return get(NODE, 4); }
     __device__ __forceinline__ uint32_t nh() const { return get(NH, 5); }
-    __device__ __forceinline__ uint32_t gen() const { return get(GEN, 4); }
 };
 
 template <bool COUNT, bool TAB>
@@ -2344,8 +2343,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const unsigned long long below = (1ull << lane) - 1ull;  // lanes under this one
     const uint32_t n = pa.n_pix;
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
-    const uint32_t guess = 4u + 6u * (uint32_t)pa.max_depth;  // draws of a full-length sample
-    const uint32_t galt = 4u + 6u;                             // draws of a one-bounce sample (the alternative)
+    const uint32_t g_full = 4u + 6u * (uint32_t)pa.max_depth;  // draws of a full-length sample
+    const uint32_t g_one = 4u + 6u;                             // draws of a one-bounce sample
+    const uint32_t lvl_cap = min(pa.spec_depth, 3u);            // tree levels used (option path_spec_depth)
+    const bool tree = pa.spec_alt != 0 && g_one != g_full;      // one-bounce branches too (option path_spec_alt)
     const uint32_t spp = pa.spp;
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
@@ -2354,12 +2355,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     f.s_lo = shard_begin(n, f.shard);
     f.s_hi = shard_begin(n, f.shard + 1);
 
-    // owner: the committed state, the start of the last main-line sample started, the next sample to
-    // commit / to start on the main line (nseq - cseq in flight, spp - nseq not started), its group's
-    // lanes; every group lane: the pixel, and the sample it runs (its state, start, number, generation)
-    uint32_t pix = 0, C = 0, tstart = 0, cseq = 0, nseq = 0;
+    // owner: the committed state and count, the tree nodes in flight (bit per node), its group's
+    // lanes; every group lane: the pixel, and the sample it runs
+    uint32_t pix = 0, C = 0, cseq = 0, occ = 0;
     unsigned long long grp = 0;
-    uint32_t seed = 0, sstart = 0, mseq = 0, mgen = 0;
+    uint32_t seed = 0;
     int depth = 0;
     V3 beta{1.0f, 1.0f, 1.0f}, Lr{0.0f, 0.0f, 0.0f}, scol{0.0f, 0.0f, 0.0f};
     float4 pe0 = {}, pe1 = {};  // extension ray waiting behind the shadow ray
@@ -2452,103 +2452,88 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 }
             }
             if (COUNT) p_tsh += wall_clock64() - p_ts;
-            // 2. commits, in sample order: each group lane compares its sample with its owner's next
-            // commit; one head per group per round
-            const bool in_grp = s.role() != ROLE_FREE;
+            // 2. commits, in sample order: a finished head is committed and its length picks the
+            // branch of the tree that moves up; rounds until no group has a finished head
             const int ol = s.role() == ROLE_HELPER ? (int)s.ol() : (int)lane;
-            for (int it = 0; it <= (int)kSpecHelpers; it++) {
-                const uint32_t o_cseq = (uint32_t)__shfl((int)cseq, ol);
-                const uint32_t o_C = (uint32_t)__shfl((int)C, ol);
-                SpecState os;
-                os.w = (uint32_t)__shfl((int)s.w, ol);
-                const uint32_t g0 = os.gen();
-                const bool mine = in_grp && (s.srun() || s.send()) &&
-                                  (mgen == g0 || (s.malt() && mgen == ((g0 + 1u) & 15u)));
-                const bool cand = mine && mseq == o_cseq;  // a candidate for the head
-                const bool valid = cand && sstart == o_C;   // ... that starts from C
-                const unsigned long long cbm = __ballot(cand), vm = __ballot(valid);
-                if (cbm == 0) break;
-                // owners: their valid candidate's lane (every lane shuffles from it, or from itself)
-                const bool act = s.role() == ROLE_OWNER && (grp & cbm) != 0;
-                const unsigned long long v = grp & vm;
-                const int hl = act && v ? __ffsll((long long)v) - 1 : (int)lane;
+            for (int it = 0; it <= (int)kSpecNodes; it++) {
+                const bool hd = s.role() != ROLE_FREE && s.send() && s.node() == 0u;  // a finished head
+                const unsigned long long hm = __ballot(hd);
+                if (hm == 0) break;
+                const bool act = s.role() == ROLE_OWNER && (grp & hm) != 0;
+                const int hl = act ? __ffsll((long long)(grp & hm)) - 1 : (int)lane;
                 V3 L;
                 L.x = __shfl(Lr.x, hl);
                 L.y = __shfl(Lr.y, hl);
                 L.z = __shfl(Lr.z, hl);
                 const uint32_t E = (uint32_t)__shfl((int)seed, hl);
-                const uint32_t hflags = (uint32_t)__shfl((int)((s.send() ? 1u : 0u) | (mgen == g0 ? 0u : 2u)), hl);
                 uint32_t hcc = 0, hcs = 0;
                 if (COUNT) {
                     hcc = (uint32_t)__shfl((int)sc_closest, hl);
                     hcs = (uint32_t)__shfl((int)sc_shadow, hl);
                 }
-                bool changed = false;
-                if (act) {
-                    if (v == 0) {  // no candidate starts from C: drop the main line and the alternative
-                        s.set(SpecState::GEN, 4, g0 + 2u);
-                        s.set(SpecState::ALT, 1, 0);
-                        nseq = cseq;
-                        changed = true;
+                uint32_t br = BR_NOCOMMIT;
+                if (act) {  // Tile::add_sample, C = the head's end state
+                    float4 fm = pa.film[pix];  // the film sums live in the (zeroed) film slot
+                    splat_one(fm, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
+                    pa.film[pix] = fm;
+                    if (COUNT) {
+                        pc_closest += hcc;
+                        pc_shadow += hcs;
+                    }
+                    br = E == lcg_advance(C, g_full) ? BR_FULL : (E == lcg_advance(C, g_one) ? BR_ONE : BR_NONE);
+                    C = E;
+                    cseq++;
+                    // the nodes on branch br move up a level, the others go
+                    uint32_t nocc = 0;
+                    for (uint32_t nd = 1; nd < kSpecNodes; nd++) {
+                        const uint32_t lv = node_lvl(nd), cd = node_code(nd);
+                        if (((occ >> nd) & 1u) && br != BR_NONE && (cd & 1u) == br)
+                            nocc |= 1u << ((1u << (lv - 1u)) - 1u + (cd >> 1));
+                    }
+                    occ = nocc;
+                }
+                const uint32_t obr = (uint32_t)__shfl((int)br, ol);
+                if (s.role() != ROLE_FREE && obr != BR_NOCOMMIT && (s.srun() || s.send())) {
+                    const uint32_t nd = s.node();
+                    bool drop = false;
+                    if (nd == 0u) {  // the committed head: its lane is free
+                        s.set(SpecState::SEND, 1, 0);
+                    } else if (obr == BR_NONE || (node_code(nd) & 1u) != obr) {
+                        drop = true;
                     } else {
-                        if (hflags & 2u) {  // the alternative starts from C: it becomes the main line
-                            s.set(SpecState::GEN, 4, g0 + 1u);
-                            s.set(SpecState::ALT, 1, 0);
-                            nseq = cseq + 1u;
-                            tstart = o_C;
-                            changed = true;
-                        } else if (s.alt() && (grp & cbm & ~vm)) {  // the main line holds: the alternative goes
-                            s.set(SpecState::ALT, 1, 0);
-                            changed = true;
-                        }
-                        if (hflags & 1u) {  // the head ended: Tile::add_sample, C = its end state
-                            float4 fm = pa.film[pix];  // the film sums live in the (zeroed) film slot
-                            splat_one(fm, make_float4(L.x, L.y, L.z, 0.0f), pa.ray_clamp);
-                            pa.film[pix] = fm;
-                            if (COUNT) {
-                                pc_closest += hcc;
-                                pc_shadow += hcs;
-                            }
-                            C = E;
-                            cseq++;
-                            changed = true;
-                        }
+                        s.set(SpecState::NODE, 4, (1u << (node_lvl(nd) - 1u)) - 1u + (node_code(nd) >> 1));
+                    }
+                    if (drop) {  // a dropped sample: its ray goes with it
+                        if (COUNT) n_abort++;
+                        s.set(SpecState::SRUN, 1, 0);
+                        s.set(SpecState::SEND, 1, 0);
+                        s.set(SpecState::PEND, 1, 0);
+                        fresh = false;
+                        busy = false;
                     }
                 }
-                if (__ballot(changed) == 0) break;
             }
-            // each group lane: its sample committed or dropped -> idle; a pixel that is done frees
-            // its group
+            // a pixel that is done frees its group
             {
-                if (s.role() == ROLE_OWNER && cseq == spp) {  // the pixel is done
+                if (s.role() == ROLE_OWNER && cseq == spp) {
                     if (pa.probe)
                         pa.probe[pix] = make_uint4(C, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u, probe_flags<COUNT>(pa));
                     s.set(SpecState::ROLE, 2, ROLE_FREE);
                     s.set(SpecState::NH, 5, 0);
-                    s.set(SpecState::ALT, 1, 0);
                     grp = 0;
+                    occ = 0;
                 }
                 SpecState os;
                 os.w = (uint32_t)__shfl((int)s.w, ol);
-                const uint32_t o_cseq = (uint32_t)__shfl((int)cseq, ol);
                 const uint32_t o_pix = (uint32_t)__shfl((int)pix, ol);
                 if (s.role() == ROLE_HELPER && (os.role() != ROLE_OWNER || o_pix != pix))
                     s.set(SpecState::ROLE, 2, ROLE_FREE);  // its pixel is done (its lane may own another)
-                const uint32_t g0 = os.gen();
-                if (s.malt() && mgen == g0) s.set(SpecState::MALT, 1, 0);  // an alternative that became the main line
-                const bool is_main = mgen == g0;
-                const bool is_alt = s.malt() && mgen == ((g0 + 1u) & 15u);
-                const bool had = s.srun() || s.send();
-                const bool gone = had && (s.role() == ROLE_FREE || (!is_main && !is_alt) ||
-                                          (is_main && mseq < o_cseq) || (is_alt && (!os.alt() || mseq < o_cseq)));
-                if (gone) {
-                    const bool committed = s.role() != ROLE_FREE && is_main && mseq < o_cseq;
-                    if (COUNT && !committed) n_abort++;
+                if (s.role() == ROLE_FREE && (s.srun() || s.send())) {  // none is left past the last sample
+                    if (COUNT) n_abort++;
                     s.set(SpecState::SRUN, 1, 0);
                     s.set(SpecState::SEND, 1, 0);
                     s.set(SpecState::PEND, 1, 0);
-                    s.set(SpecState::MALT, 1, 0);
-                    fresh = false;  // a dropped sample's ray goes with it
+                    fresh = false;
                     busy = false;
                 }
             }
@@ -2560,20 +2545,21 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 if (asked && !need) {
                     const uint32_t px = pa.pixel[pix];
                     C = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
-                    cseq = nseq = 0;
+                    cseq = 0;
+                    occ = 0;
                     grp = 1ull << lane;
                     s.set(SpecState::ROLE, 2, ROLE_OWNER);
-                    s.set(SpecState::ALT, 1, 0);
                     s.set(SpecState::NH, 5, 0);
                     if (COUNT) pc_closest = pc_shadow = 0;
                 }
             }
-            // 4. lanes with nothing left to fetch join the groups of owners with samples to start, one
-            // per owner per phase; the owners with at least half the wave's most samples left first
+            // 4. lanes with nothing left to fetch join the groups of owners with samples to speculate
+            // on, one per owner per phase; the owners with at least half the wave's most samples left
+            // first
             {
+                const uint32_t left = spp - cseq;  // samples not committed
                 const bool avail = s.role() == ROLE_FREE && done;
-                const uint32_t left = spp - nseq;  // main-line samples not started
-                const bool want = s.role() == ROLE_OWNER && s.nh() < min(kSpecHelpers, pa.spec_depth + 1u) && left > 0;
+                const bool want = s.role() == ROLE_OWNER && s.nh() < (tree ? (2u << lvl_cap) - 2u : lvl_cap) && left > 1u;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
                 int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
@@ -2604,63 +2590,47 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     pix = np;
                 }
             }
-            // 5. starts: the idle lanes of a group take the next main-line samples in lane order (the
-            // first from C when nothing is in flight, every other from the guessed state one full-length
-            // sample on; at most spec_depth beyond the head), then one more may take the alternative
+            // 5. starts: the idle lanes of a group take the free nodes in order of expected use, the
+            // head first (from C); a node l levels down starts after its l assumed sample lengths
             {
                 const int ol2 = s.role() == ROLE_HELPER ? (int)s.ol() : (int)lane;
                 const bool idle = s.role() != ROLE_FREE && !s.srun() && !s.send();
                 const unsigned long long im = __ballot(idle);
-                uint32_t cnt = 0, zero = 0, base = 0, seq0 = 0, ago = 0, astart = 0;
+                unsigned long long pick = 0;  // the nodes handed out, one per nibble, in idle-lane order
+                uint32_t npick = 0;
                 if (s.role() == ROLE_OWNER) {
                     const uint32_t nfree = (uint32_t)__popcll(grp & im);
-                    const uint32_t inflight = nseq - cseq, cap = 1u + pa.spec_depth;
-                    cnt = min(min(nfree, spp - nseq), cap > inflight ? cap - inflight : 0u);
-                    zero = inflight == 0 ? 1u : 0u;
-                    base = zero ? C : tstart;
-                    seq0 = nseq;
-                    if (cnt) {
-                        tstart = lcg_advance(base, guess * (cnt - zero));  // the last new sample's start
-                        nseq += cnt;
-                    }
-                    if (pa.spec_alt && !s.alt() && nfree > cnt && nseq > cseq && cseq + 1u < spp && galt != guess) {
-                        ago = 1;
-                        astart = lcg_advance(C, galt);  // the sample after a one-bounce head
-                        s.set(SpecState::ALT, 1, 1);
+                    const uint32_t lv_max = min(lvl_cap, spp - cseq - 1u);  // nodes past the last sample are useless
+                    for (uint32_t k = 0; k < kSpecNodes && npick < nfree; k++) {
+                        const uint32_t nd = (uint32_t)(kSpecNodeOrder >> (4u * k)) & 15u;
+                        if (((occ >> nd) & 1u) || node_lvl(nd) > lv_max || (node_code(nd) && !tree)) continue;
+                        pick |= (unsigned long long)nd << (4u * npick);
+                        npick++;
+                        occ |= 1u << nd;
                     }
                 }
-                const uint32_t o_cnt = (uint32_t)__shfl((int)cnt, ol2);
-                const uint32_t o_zero = (uint32_t)__shfl((int)zero, ol2);
-                const uint32_t o_base = (uint32_t)__shfl((int)base, ol2);
-                const uint32_t o_seq0 = (uint32_t)__shfl((int)seq0, ol2);
-                const uint32_t o_ago = (uint32_t)__shfl((int)ago, ol2);
-                const uint32_t o_astart = (uint32_t)__shfl((int)astart, ol2);
-                const uint32_t o_cseq = (uint32_t)__shfl((int)cseq, ol2);
-                const uint32_t o_gen = ((uint32_t)__shfl((int)s.w, ol2) >> SpecState::GEN) & 15u;
+                const uint32_t o_np = (uint32_t)__shfl((int)npick, ol2);
+                const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)pick, ol2);
+                const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)(pick >> 32), ol2);
+                const uint32_t o_C = (uint32_t)__shfl((int)C, ol2);
                 const uint32_t glo = (uint32_t)__shfl((int)(uint32_t)grp, ol2);
                 const uint32_t ghi = (uint32_t)__shfl((int)(uint32_t)(grp >> 32), ol2);
-                if (idle && (o_cnt || o_ago)) {
+                if (idle && o_np) {
                     const unsigned long long og = ((unsigned long long)ghi << 32) | glo;
                     const uint32_t k = (uint32_t)__popcll(og & im & below);  // this lane's rank among the idle
-                    if (k < o_cnt) {
-                        const uint32_t ahead = k + 1u - o_zero;  // full-length samples between base and this start
-                        seed = ahead ? lcg_advance(o_base, guess * ahead) : o_base;
-                        if (COUNT && ahead) n_spec++;
-                        mseq = o_seq0 + k;
-                        mgen = o_gen;
-                        start = true;
-                    } else if (o_ago && k == o_cnt) {  // the alternative, one generation on
-                        seed = o_astart;
-                        if (COUNT) n_spec++;
-                        mseq = o_cseq + 1u;
-                        mgen = (o_gen + 1u) & 15u;
-                        s.set(SpecState::MALT, 1, 1);
+                    if (k < o_np) {
+                        const unsigned long long pk = ((unsigned long long)phi << 32) | plo;
+                        const uint32_t nd = (uint32_t)(pk >> (4u * k)) & 15u;
+                        const uint32_t lv = node_lvl(nd), cd = node_code(nd), ones = (uint32_t)__popc(cd);
+                        const uint32_t ahead = (lv - ones) * g_full + ones * g_one;
+                        seed = ahead ? lcg_advance(o_C, ahead) : o_C;
+                        if (COUNT && lv) n_spec++;
+                        s.set(SpecState::NODE, 4, nd);
                         start = true;
                     }
                 }
                 if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
                     const uint32_t px = pa.pixel[pix];
-                    sstart = seed;
                     Lr = V3{0.0f, 0.0f, 0.0f};
                     beta = V3{1.0f, 1.0f, 1.0f};
                     depth = 0;

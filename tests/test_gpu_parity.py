@@ -621,13 +621,15 @@ def _tab_fits(cs):
 @pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
                                                       (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
                                                       (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2),
-                                                      (1, 2, 0, 1, 0), (1, 2, 0, 0, 2), (1, 2, 0, 1, 2)])
+                                                      (1, 2, 0, 1, 0), (1, 2, 0, 0, 2), (1, 2, 0, 1, 2),
+                                                      (1, 3, 0, 1, 0), (1, 3, 0, 1, 2), (1, 4, 0, 0, 0)])
 def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab, order):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
     §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
     scrambled or tile-order pixel fetch; defer = 1), its speculative-sample form (k_path_spec, §3.11:
     idle lanes run a busy pixel's next sample from a guessed sampler state, committed in order only
-    when the guess was the true state; defer = 2) and the wavefront kernels give the oracle's image bit for
+    when the guess was the true state; defer = 2, 3 with the speculation tree's one-bounce branches, 4
+    with one sample beyond the head) and the wavefront kernels give the oracle's image bit for
     bit: ragged / clipped / empty tiles, depths 0-9 (above 8 the deferred form falls back to
     k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
     deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes); with the
@@ -636,7 +638,9 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
     def opts(ctx):
         ctx.set_option("path", path)
         ctx.set_option("path_defer", 1 if defer == 1 else 0)
-        ctx.set_option("path_spec", 1 if defer == 2 else 0)
+        ctx.set_option("path_spec", 1 if defer >= 2 else 0)
+        ctx.set_option("path_spec_alt", 1 if defer == 3 else 0)
+        ctx.set_option("path_spec_depth", 1 if defer == 4 else 3)
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
         ctx.set_option("path_order", order)
