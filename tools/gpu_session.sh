@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU-box session: each GPU step has its own time limit; the script stops at the first step that
-# faults, aborts, segfaults or times out (exit codes other than 0/1), and never retries.
+# fails (a test failure, a fault, an abort, a segfault or a time limit: a pytest thread timeout
+# leaves its kernel running), and never retries.
 # Usage: tools/gpu_session.sh "<step-name> <seconds> <command>" ...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -14,7 +15,7 @@ for spec in "$@"; do
     rc=$?
     echo "=== [$name] rc=$rc after $(( $(date +%s) - start ))s" | tee -a gpurun_out/session.log
     tail -n 25 "gpurun_out/$name.log"
-    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    if [ $rc -ne 0 ]; then
         echo "=== stopping: step $name ended with rc=$rc" | tee -a gpurun_out/session.log
         exit $rc
     fi
