@@ -317,6 +317,11 @@ struct akr_hip_ctx {
     // option "path_order_sub": one pilot ray per 2^path_order_sub slots (neighbours in a tile row
     // share its cost); 0 = a pilot ray per slot
     int path_order_sub = 0;
+    // option "path_order_pilot_spp": S > 0 ranks slots by the rays their first S samples take in a
+    // counting k_path render (a path pilot; nothing of it reaches the film or the sampler states)
+    // instead of one pilot camera ray's steps (0, default)
+    int path_order_pilot_spp = 0;
+    DBuf<uint4> d_pprobe;  // the path pilot's per-slot probe
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
     DBuf<TraceCounters> d_ocnt;
@@ -765,6 +770,32 @@ struct akr_hip_ctx {
         HIPCHK(hipGetLastError());
     }
 
+    // Path pilot: a counting k_path render of S samples per slot (the render's own first samples: a
+    // slot's sampler starts from its seed in every render) into the zeroed film, whose probe gives
+    // each slot's rays; the film is zeroed again for the render.  Classes of 2^shift rays.
+    void pixel_order_path(const PathArgs &base, bool tab, uint32_t grid, uint32_t N, int S, hipStream_t ms) {
+        if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
+        d_pprobe.reserve(N);
+        HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
+        PathArgs pp = base;
+        pp.spp = (uint32_t)S;
+        pp.work = d_owork.p;
+        pp.t.counters = d_ocnt.p;
+        pp.prof = nullptr;
+        pp.probe = d_pprobe.p;
+        pp.probe_clock = 0;
+        pp.order = nullptr;
+        pp.fault_test = 0;
+        launch_path(true, PATH_PLAIN, tab, pp, std::min<uint32_t>(grid, path_grid[PATH_PLAIN][tab]), ms);
+        launch_probe_cost(d_pprobe.p, N, d_okey[1].p, ms);
+        HIPCHK(hipMemsetAsync(d_film.p, 0, (size_t)N * sizeof(float4), ms));
+        uint32_t shift = 0;  // at most ~9 rays per sample (max_depth 5: 5 closest-hit + 4 shadow)
+        while (((uint32_t)(9 * S + 1) >> shift) > (uint32_t)path_order_classes) shift++;
+        launch_order_keys(d_okey[1].p, N, shift, (uint32_t)(path_order_classes - 1), 0, d_okey[0].p, d_oidx[0].p, ms);
+        sort_pixel_order(d_otmp.p, d_otmp.n, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
+        HIPCHK(hipGetLastError());
+    }
+
     // Pixels of the tile list (tiles in order, row-major inside a tile) into d_pixel, expanded on
     // the device from the clipped tiles (the host loop over every pixel and the pageable upload of
     // its list cost 1.7 ms per 1080p render); sizes the queues and the per-pass counter sets.
@@ -1031,7 +1062,10 @@ struct akr_hip_ctx {
                                               ? std::min(path_order_share_min_spp, path_order_min_spp)
                                               : path_order_min_spp;
                 if (path_order != 0 && (kind == PATH_PLAIN || path_order == 2) && p.spp >= order_min_spp && N >= 2) {
-                    timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
+                    if (path_order_pilot_spp > 0)
+                        timed("pilot", ms, [&] { pixel_order_path(pa, tab, grid, (uint32_t)N, path_order_pilot_spp, ms); });
+                    else
+                        timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
                     pa.order = d_oidx[1].p;
                     const bool pair = path_order_pair == 3 ||
                                       (kind != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000)));
@@ -1379,6 +1413,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec") {
             if (value < 0 || value > 2) throw std::runtime_error("path_spec must be 0, 1 or 2");
             ctx->path_spec = (int)value;
+        } else if (k == "path_order_pilot_spp") {
+            if (value < 0 || value > 64) throw std::runtime_error("path_order_pilot_spp must be in [0, 64]");
+            ctx->path_order_pilot_spp = (int)value;
         } else if (k == "path_spec_alt") {
             ctx->path_spec_alt = value != 0;
         } else if (k == "path_spec_depth") {

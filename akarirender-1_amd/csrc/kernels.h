@@ -31,6 +31,7 @@ void launch_merge_film(const float4 *film, const uint32_t *pixel, const uint32_t
 void launch_unpack(const float4 *film, uint32_t n, float *rad, float *w, hipStream_t st);
 void launch_expand_pixels(const uint4 *tiles, uint32_t n_tiles, uint32_t n, uint32_t *pixel, hipStream_t st);
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st);
+void launch_probe_cost(const uint4 *probe, uint32_t n, uint32_t *cost, hipStream_t st);
 // cost-ordered pixel fetch: pilot camera rays, sort keys, and the stable key sort (lbvh.hip, rocPRIM)
 // 5-bit cost classes (31 = the costliest, with the rays the pilot does not trace): with the shard's 3 bits
 // the key is one byte, so the radix sort is a single 8-bit pass (12-bit classes took 17 kernel launches,

@@ -2784,6 +2784,13 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, ui
     idx[i] = i;
 }
 
+// Path pilot (option path_order_pilot_spp): a slot's cost is the rays (closest-hit + shadow) its first
+// samples took in a counting render, from the pixel probe of that render
+__global__ __launch_bounds__(kBlock) void k_probe_cost(const uint4 *probe, uint32_t n, uint32_t *cost) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) cost[i] = probe[i].y + probe[i].z;
+}
+
 // one word from device memory into mapped host memory (the host polls it after an event)
 // Wavefront form: the final sampler state of every slot into its pixel probe (the ray counts were
 // added by k_raygen / k_shade)
@@ -2937,6 +2944,9 @@ void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32
     if (n == 0) return;
     hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift,
                        cmax < kOrderClassMask ? cmax : kOrderClassMask, sub, key, idx);
+}
+void launch_probe_cost(const uint4 *probe, uint32_t n, uint32_t *cost, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_probe_cost, dim3(blocks_for(n)), dim3(kBlock), 0, st, probe, n, cost);
 }
 void launch_probe_seed(const uint32_t *seed, uint32_t n, uint4 *probe, hipStream_t st) {
     if (n == 0) return;

@@ -571,6 +571,32 @@ def test_kernel_stats_modes(hip_ctx_factory):
         ctx.set_option("stats", 0)
 
 
+@pytest.mark.parametrize("defer", [0, 1, 2])
+def test_path_pilot_order_bit_exact(hip_ctx_factory, defer):
+    """The path pilot (option path_order_pilot_spp): slots ranked by the rays of
+    their first samples in a counting k_path render, which must leave nothing behind: the ordered
+    render of every persistent form equals the oracle bit for bit, film, weights, sampler states and
+    (counting build) ray counts per pixel."""
+    with hip_ctx_factory(0) as ctx:
+        ctx.set_option("path", 1)
+        ctx.set_option("path_defer", 1 if defer == 1 else 0)
+        ctx.set_option("path_spec", 1 if defer == 2 else 0)
+        ctx.set_option("path_order", 2)
+        ctx.set_option("path_order_min_spp", 0)
+        ctx.set_option("path_order_share_min_spp", 0)
+        ctx.set_option("path_order_pilot_spp", 2)
+        cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
+        for spp, depth in ((1, 5), (6, 5), (3, 2)):
+            _check_render(ctx, orc, spp, depth, [(0, 0, 48, 27), (5, 3, 19, 11)], 48, 27, probe=True)
+            assert ctx.render_form()["ordered"]
+        try:
+            ctx.set_option("count_tests", 1)
+            *_, rays = _check_render(ctx, orc, 4, 5, [(0, 0, 48, 27)], 48, 27, probe=True)
+            assert rays
+        finally:
+            ctx.set_option("count_tests", 0)
+
+
 def test_auto_form_by_shading(hip_ctx_factory):
     """Auto dispatch: constant Diffuse / Emissive scenes render with the persistent
     kernel, scenes with Glossy / Mix materials or image textures with the wavefront (whose shade
