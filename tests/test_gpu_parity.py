@@ -157,7 +157,8 @@ def test_trace_each_ray_once(hip_ctx_factory, n):
         rays = random_rays(n, 7, -1.1, 1.1)
         ctx.set_option("count_tests", 1)
         ctx.set_option("lookahead", 1)   # no speculative lanes: exactly the sequential rays
-        for any_hit in (False, True):
+        ctx.set_option("path_spec", 0)   # (k_path_spec's dropped samples trace rays too; its
+        for any_hit in (False, True):    # committed rays are checked per pixel by the probe tests)
             ctx.reset_stats()
             ctx.trace(rays, any_hit=any_hit)
             assert ctx.trace_counts()["per_mode"]["any" if any_hit else "closest"]["rays"] == n
