@@ -255,6 +255,7 @@ struct RaygenArgs {
     uint32_t *count_out;
     int32_t first_pass;
     uint4 *probe;                  // optional, per slot (akr_pixel_probe): .y counts the camera ray
+    const uint32_t *order;         // optional: queue position -> slot (the cost order)
     uint32_t lookahead;            // nonzero: k_raygen_lanes over the planned lanes of `look`
     LookArgs look;
 };

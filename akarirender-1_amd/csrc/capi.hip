@@ -321,6 +321,9 @@ struct akr_hip_ctx {
     // counting k_path render (a path pilot; nothing of it reaches the film or the sampler states)
     // instead of one pilot camera ray's steps (0, default)
     int path_order_pilot_spp = 0;
+    // option "wave_order": the wavefront's camera rays queued in the cost order (costliest first in
+    // each shard of the closest-hit launch), by the same rule and floors as the persistent kernels
+    bool wave_order = true;
     DBuf<uint4> d_pprobe;  // the path pilot's per-slot probe
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -1088,6 +1091,21 @@ struct akr_hip_ctx {
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
         int64_t g = 0;  // bounce index over all passes: shadow queues alternate by its parity
+        const uint32_t *worder = nullptr;  // the cost order of the camera rays (option wave_order)
+        {
+            const int order_min_spp = (int64_t)N <= path_order_share_pixels
+                                          ? std::min(path_order_share_min_spp, path_order_min_spp)
+                                          : path_order_min_spp;
+            if (wave_order && path_order != 0 && !la && p.spp >= order_min_spp && N >= 2) {
+                if (!order_warm) {
+                    pixel_order((uint32_t)std::min<uint64_t>(N, 64), ms);
+                    order_warm = true;
+                }
+                timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
+                worder = d_oidx[1].p;
+            }
+            last_ordered = worder ? 1 : 0;
+        }
         for (int s = 0; s < p.spp; s++) {
             const int ps = s & 1;
             // lookahead: stop once the pass before last finished every pixel (the last pass then
@@ -1109,6 +1127,7 @@ struct akr_hip_ctx {
             HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
             RaygenArgs rg = raygen_args(la ? (uint32_t)S : (uint32_t)N, L, qcount(0), s == 0);
             rg.probe = probe_p;
+            rg.order = worder;
             if (la) {
                 rg.lookahead = 1;
                 rg.look = look(ps);
@@ -1413,6 +1432,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec") {
             if (value < 0 || value > 2) throw std::runtime_error("path_spec must be 0, 1 or 2");
             ctx->path_spec = (int)value;
+        } else if (k == "wave_order") {
+            ctx->wave_order = value != 0;
         } else if (k == "path_order_pilot_spp") {
             if (value < 0 || value > 64) throw std::runtime_error("path_order_pilot_spp must be in [0, 64]");
             ctx->path_order_pilot_spp = (int)value;

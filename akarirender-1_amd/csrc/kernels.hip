@@ -798,17 +798,20 @@ __device__ __forceinline__ void camera_ray(const CameraDev &cam, int x, int y, u
 __global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= a.n) return;
-    const uint32_t px = a.pixel[i];
+    // queue entry i holds slot sl: with the cost order the costliest camera rays are fetched first
+    // in each XCD shard of the closest-hit launch (the order's shards are the launch's shards)
+    const uint32_t sl = a.order ? a.order[i] : i;
+    const uint32_t px = a.pixel[sl];
     const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
-    uint32_t seed = a.first_pass ? (uint32_t)(x + y * a.cam.width) : a.seed[i];
+    uint32_t seed = a.first_pass ? (uint32_t)(x + y * a.cam.width) : a.seed[sl];
     float4 r0, r1;
     camera_ray(a.cam, x, y, seed, r0, r1);
-    a.L[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a.L[sl] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     a.ray_out[2 * (size_t)i] = r0;
     a.ray_out[2 * (size_t)i + 1] = r1;
     a.state_out[i] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
-    a.slot_out[i] = i;
-    if (a.probe) a.probe[i].y += 1u;  // the camera ray (always traced)
+    a.slot_out[i] = sl;
+    if (a.probe) a.probe[sl].y += 1u;  // the camera ray (always traced)
     if (i == 0) *a.count_out = a.n;
 }
 

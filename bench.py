@@ -355,7 +355,7 @@ def main():
     ap.add_argument("--slot-target", type=int, default=0, help="auto lookahead: path slots per render (0: library default)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
-    ap.add_argument("--wavefront-spp", type=int, default=8,
+    ap.add_argument("--wavefront-spp", type=int, default=16,
                     help="untimed same-run leg in the wavefront form (north_star's layout), spp; 0 = skip")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearse the N-rank path on a one-GPU box: every rank on device 0, a gloo process group, "

@@ -645,7 +645,7 @@ def _tab_fits(cs):
     return nl * 96 + nm * 48 + (nl + 1) * 4 <= 1024
 
 
-@pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
+@pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (0, 0, 0, 1, 1), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
                                                       (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
                                                       (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2),
                                                       (1, 2, 0, 1, 0), (1, 2, 0, 0, 2), (1, 2, 0, 1, 2),
@@ -661,7 +661,8 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
     k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
     deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes); with the
     scene's material / light / CDF tables read from HBM or from the kernels' LDS copy (tab); with the
-    cost-ordered pixel fetch (order, §3.10) forced on at every spp, or off."""
+    cost-ordered pixel fetch (order, §3.10; the wavefront's camera-ray queue, option wave_order)
+    forced on at every spp, or off."""
     def opts(ctx):
         ctx.set_option("path", path)
         ctx.set_option("path_defer", 1 if defer == 1 else 0)
