@@ -270,6 +270,9 @@ struct akr_hip_ctx {
     // (the 8-way share and the whole frame re-measured with the lane groups: 0.82 / 4.85 ms against
     // 0.86 / 4.61 ms for k_path_defer / k_path, profiles/r19_spec_*.log)
     int path_spec_fetch = 3;   // option "path_spec_fetch": k_path_spec's ordered fetch, FETCH_STRIDE (3); -1 = the path_order_pair rule
+    // ... for renders of at most this many pixels (the 8-way share); larger ones (2- and 4-way) take the
+    // path_order_pair rule: 2.500 / 1.399 ms against 2.526 / 1.403 strided (profiles/r20_spec_fetch_ab.log)
+    int64_t path_spec_fetch_pixels = 400000;
     int path_spec_depth = 3;   // option "path_spec_depth": samples in flight beyond a pixel's head (1-3, the
                                // speculation tree's levels; the r19 main line measured 2, 4, 8, 15 alike, 1 slower,
                                // profiles/r19_spec_depth.log)
@@ -1075,7 +1078,8 @@ struct akr_hip_ctx {
                     pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
                     // k_path_spec: every wave takes pixels from the whole cost order (FETCH_STRIDE), so
                     // each has cheap pixels whose lanes turn helpers early (option path_spec_fetch)
-                    if (kind == PATH_SPEC && path_spec_fetch >= 0) pa.order_mode = (uint32_t)path_spec_fetch;
+                    if (kind == PATH_SPEC && path_spec_fetch >= 0 && (int64_t)N <= path_spec_fetch_pixels)
+                        pa.order_mode = (uint32_t)path_spec_fetch;
                     pa.prio = (uint32_t)path_prio;
                 }
                 timed("path", ms, [&] { launch_path(count, kind, tab, pa, grid, ms); });
@@ -1442,6 +1446,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec_depth") {
             if (value < 1 || value > 3) throw std::runtime_error("path_spec_depth must be in [1, 3]");
             ctx->path_spec_depth = (int)value;
+        } else if (k == "path_spec_fetch_pixels") {
+            if (value < 0) throw std::runtime_error("path_spec_fetch_pixels must be >= 0");
+            ctx->path_spec_fetch_pixels = value;
         } else if (k == "path_spec_fetch") {
             if (value < -1 || value > 3) throw std::runtime_error("path_spec_fetch must be in [-1, 3]");
             ctx->path_spec_fetch = (int)value;
