@@ -361,7 +361,10 @@ struct akr_hip_ctx {
     bool stats_closest_only = false;  // time trace_closest only (HIP events on every launch cost ~7 % at small ranks)
     bool exact_cull = false;  // true: the reference intersectAABB (no behind-origin cull)
     int rays_per_lane = 1;    // trace grid sizing: at least this many queued rays per lane
-    int shadow_grid_pct = 100;  // persistent shadow-trace grid as a percentage of the resident maximum
+    // persistent shadow-trace grid as a percentage of the resident maximum: the shadow trace runs beside
+    // the next closest-hit trace, and 75 % leaves it room (wavefront 5.368 / 5.353 ms per spp against
+    // 5.400 / 5.389 at 100 %, 5.395 / 5.380 at 50 %; profiles/r20_shadow_grid_ab.log)
+    int shadow_grid_pct = 75;
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
     int wide_collapse = AKR_COLLAPSE_SAH;  // akr_build_params::wide_collapse of the last build

@@ -20,8 +20,9 @@ for k in range(max(counts)):
     scene.upload_scene(c, cs, n_threads=16)
     ctxs.append(c)
 tiles = tiles_for_rank(W, H, 32, 0, 1)
-for opts in ({}, {"rays_per_lane": 2}, {"shadow_grid_pct": 50}):
+for opts in ({"path": 0}, {"path": 0, "shadow_grid_pct": 50}, {"path": 2}):
     for c in ctxs:
+        c.set_option("path", opts.get("path", 2))   # 0: the wavefront (north_star's layout)
         c.set_option("rays_per_lane", opts.get("rays_per_lane", 1))
         c.set_option("shadow_grid_pct", opts.get("shadow_grid_pct", 100))
     for n in counts:
