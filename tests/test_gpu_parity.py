@@ -598,6 +598,22 @@ def test_path_pilot_order_bit_exact(hip_ctx_factory, defer):
             ctx.set_option("count_tests", 0)
 
 
+def test_spec_and_order_options_are_validated(hip_ctx_factory):
+    """The speculative form's and the cost order's options reject values outside their ranges
+    (akr_hip_set_option returns an error and leaves the option as it was), and accept their ends."""
+    with hip_ctx_factory(0) as ctx:
+        for key, good, bad in (("path_spec_depth", (1, 3), (0, 4)), ("path_spec_fetch", (-1, 3), (-2, 5)),
+                               ("path_order_pilot_spp", (0, 64), (-1, 65)), ("path_spec_fetch_pixels", (0, 1 << 40), (-1,)),
+                               ("wave_order", (0, 1), ()), ("path_spec_alt", (0, 1), ())):
+            for v in good:
+                ctx.set_option(key, v)
+            for v in bad:
+                with pytest.raises(capi.AkrError, match=key):
+                    ctx.set_option(key, v)
+        with pytest.raises(capi.AkrError):
+            ctx.set_option("no_such_option", 1)
+
+
 def test_auto_form_by_shading(hip_ctx_factory):
     """Auto dispatch: constant Diffuse / Emissive scenes render with the persistent
     kernel, scenes with Glossy / Mix materials or image textures with the wavefront (whose shade
