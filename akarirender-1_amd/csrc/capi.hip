@@ -311,8 +311,9 @@ struct akr_hip_ctx {
     int path_order_share_min_spp = 16;
     int path_order_shift = 2;
     // option "path_order_classes": at most this many cost classes (1..32), the costliest holding every
-    // pixel above; fewer classes keep more of the tile order inside a shard
-    int path_order_classes = 32;
+    // pixel above; fewer classes keep more of the tile order inside a shard (16 since r20: whole frame
+    // 4.612 against 4.627 ms per spp, 8-way share 0.803 against 0.808, profiles/r20_order_classes_ab.log)
+    int path_order_classes = 16;
     // option "path_order_cap": a pilot ray stops after this many steps (0: none); its cost class is
     // then the cap's.  The pilot is a small latency-bound launch whose length is set by its slowest
     // ray, while the order only needs coarse classes (soup against background).
