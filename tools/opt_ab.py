@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--ranks", default="0", help="ranks of the split to time (comma list; 'all')")
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--tris", type=int, default=10_000_000)
+    ap.add_argument("--tile", type=int, default=64, help="tile size of the split (bench.py's default; 32 before r20)")
     ap.add_argument("--configs", nargs="+", default=[""])
     args = ap.parse_args()
     import torch
@@ -55,7 +56,7 @@ def main():
     film = torch.zeros(4 * W * H, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     ranks = list(range(args.split)) if args.ranks == "all" else [int(r) for r in args.ranks.split(",")]
-    shares = {r: (dist.tile_grid(W, H, 32) if args.split == 1 else dist.tiles_for_rank(W, H, 32, r, args.split))
+    shares = {r: (dist.tile_grid(W, H, args.tile) if args.split == 1 else dist.tiles_for_rank(W, H, args.tile, r, args.split))
               for r in ranks}
 
     def run(c, tiles, spp):
