@@ -155,6 +155,7 @@ EXPORTS = {
     "akr_hip_render_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "akr_hip_synchronize": (C.c_int, [_P]),
     "akr_hip_render_form": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "akr_hip_render_form_inputs": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "akr_hip_pixel_probe": (C.c_int, [_P, _P, C.c_uint64]),
     "akr_bvh_host_build": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, C.POINTER(BuildParams), C.POINTER(_P),
                                      C.POINTER(AccelInfo)]),
@@ -472,6 +473,13 @@ class HipContext:
         f, o = C.c_int32(0), C.c_int32(0)
         self._check(self.lib.akr_hip_render_form(self.h, C.byref(f), C.byref(o)))
         return {"form": FORM_NAMES.get(f.value, str(f.value)), "ordered": bool(o.value)}
+
+    def render_form_inputs(self) -> dict:
+        """The last persistent render's form-choice inputs: pixels per resident lane,
+        and the pilot's rays and misses (-1: the choice did not read the pilot)."""
+        a, b, c = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        self._check(self.lib.akr_hip_render_form_inputs(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"pixels_per_lane": a.value / 1000, "pilot_rays": b.value, "pilot_misses": c.value}
 
     def path_profile(self) -> dict:
         """k_path phase profile of the counted launches since reset_stats (ticks: 100 MHz)."""

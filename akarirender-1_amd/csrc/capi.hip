@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -254,34 +255,49 @@ struct akr_hip_ctx {
     uint32_t ovf_threads = 0;
     uint32_t trace_grid[3] = {0, 0, 0};
     uint32_t path_grid[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // resident workgroups of the persistent path kernels [kind][tab]
-    // option "path_defer": 1 = k_path_defer (max_depth <= 8), 0 = k_path, 2 (default) = k_path_defer for
-    // renders of at most path_defer_pixels pixels (measured on C3, DESIGN.md §3.9: 13 % faster on an
-    // 8-way share and 4 % on a 4-way one, 1 % slower on a 2-way share and 5 % on the whole frame,
-    // whose lanes seldom have spare capacity)
+    // The render form of a constant-shading scene.  A "tail form"
+    // (k_path_spec, or k_path_defer when path_spec is 0) pays where k_path's launch would end on a few
+    // long pixel chains while most lanes idle: few pixels per resident lane, and many pixels whose
+    // paths end at once (the camera ray leaves the scene), whose lanes then free up early.  Both come
+    // from the render itself: pixels per resident lane from the occupancy query, the share of camera
+    // rays that miss from the cost-ordering pilot (which marks them).  A render without a pilot
+    // (below the order's spp floor, or path_order 0) runs k_path.
+    // option "path_defer": 1 = k_path_defer (max_depth <= 8), 0 = k_path, 2 (default) = the rule above
     int path_defer = 2;
     // option "path_spec": k_path_spec (lanes left idle by the drained pixel queue run
-    // the next sample of a busy pixel from a guessed sampler state; committed in order, bit-exact):
-    // 1 = always, 0 = never, 2 (default) = for renders of at most path_spec_pixels pixels of scenes of at
-    // least path_defer_min_tris triangles, where it replaces k_path_defer (measured on C3 at 1040 spp:
-    // 8-way share 0.89 -> 0.83 ms per spp, 2-way 2.55 -> 2.48, 4-way unchanged, the whole frame 2 %
-    // slower, profiles/r19_spec_ab.log)
+    // later samples of a busy pixel from guessed sampler states; committed in order, bit-exact):
+    // 1 = always, 0 = never (the rule's tail form is then k_path_defer), 2 (default) = the tail form
+    // when path_defer is 2.  Measured on C3 at 1040 spp: 8-way share 0.89 -> 0.83 ms per spp against
+    // k_path_defer, 2-way 2.55 -> 2.48 against k_path, the whole frame 5 % slower (profiles/r19_spec_*.log)
     int path_spec = 2;
-    int64_t path_spec_pixels = 1200000;
-    // (the 8-way share and the whole frame re-measured with the lane groups: 0.82 / 4.85 ms against
-    // 0.86 / 4.61 ms for k_path_defer / k_path, profiles/r19_spec_*.log)
+    // option "path_tail_ppl10": tail forms only at most path_tail_ppl10 / 10 pixels per resident lane
+    // (default 6.0).  1080p C3 on one MI355X: the whole frame has 7.9 pixels per lane (k_path 4.61 ms
+    // against 4.85 for k_path_spec), a 2-way share 4.0 (2.55 against 2.48)
+    int64_t path_tail_ppl10 = 60;
+    // option "path_tail_miss_pct": ... and at least this share (percent) of pilot camera rays missing
+    // the scene (C3 shares: ~45 %; the Cornell box at 1080p: 2.5-4.7 % per 8-way share, the frame's
+    // edges beside the box, where k_path runs an 8-way share in 0.276 ms against 0.300 for
+    // k_path_defer, profiles/r16_cornell_forms.log)
+    int path_tail_miss_pct = 15;
+    // explicit overrides of the rule's size test (0, default: pixels per lane): a tail form for renders
+    // of at most this many pixels (options "path_spec_pixels", "path_defer_pixels"); option
+    // "path_defer_min_tris" (0, default: no test) keeps scenes below it on k_path
+    int64_t path_spec_pixels = 0;
+    int64_t path_defer_pixels = 0;
+    int64_t path_defer_min_tris = 0;
     int path_spec_fetch = 3;   // option "path_spec_fetch": k_path_spec's ordered fetch, FETCH_STRIDE (3); -1 = the path_order_pair rule
-    // ... for renders of at most this many pixels (the 8-way share); larger ones (2- and 4-way) take the
-    // path_order_pair rule: 2.500 / 1.399 ms against 2.526 / 1.403 strided (profiles/r20_spec_fetch_ab.log)
-    int64_t path_spec_fetch_pixels = 400000;
+    // ... for renders of at most 1.5 pixels per resident lane (the 8-way share) or, when set, at most
+    // path_spec_fetch_pixels pixels; larger ones (2- and 4-way) take the path_order_pair rule: 2.500 /
+    // 1.399 ms against 2.526 / 1.403 strided (profiles/r20_spec_fetch_ab.log)
+    int64_t path_spec_fetch_pixels = 0;
     int path_spec_depth = 3;   // option "path_spec_depth": samples in flight beyond a pixel's head (1-3, the
                                // speculation tree's levels; the r19 main line measured 2, 4, 8, 15 alike, 1 slower,
                                // profiles/r19_spec_depth.log)
     bool path_spec_alt = false;  // option "path_spec_alt": the tree's one-bounce branches too (measured slower)
-    int64_t path_defer_pixels = 600000;
-    // auto takes k_path_defer only for scenes of at least this many triangles: in a tiny scene a
-    // shadow ray costs less than handing it over (Cornell box 8-way share: k_path 0.276 ms against
-    // 0.300 ms; a 100K-triangle soup: 0.665 against 0.571 ms)
-    int64_t path_defer_min_tris = 10000;
+    // the last render's form inputs (akr_hip_render_form_inputs): pixels per lane x 1000, pilot rays, misses
+    int64_t last_ppl1000 = 0, last_pilot_rays = -1, last_pilot_miss = -1;
+    DBuf<uint32_t> d_miss;        // the pilot's miss count
+    uint32_t *h_miss = nullptr, *d_miss_host = nullptr;  // mapped host word it is copied into
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
     // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
@@ -293,8 +309,8 @@ struct akr_hip_ctx {
     int path_order = 2;
     // option "path_order_pair": the cost-ordered fetch of k_path_defer pairs each shard's costliest
     // pixels with its cheapest inside a wave (lanes done early take the long pixels' shadow rays)
-    // instead of costliest-first: 1 = on, 0 = off, 3 = on for k_path too, 2 (default) = on for renders of at most 400 K
-    // pixels (measured on C3 at 32 spp, DESIGN.md §3.10: 8-way share 1.007 -> 0.946 ms, 4-way share
+    // instead of costliest-first: 1 = on, 0 = off, 3 = on for k_path too, 2 (default) = on for renders of at most
+    // 1.5 pixels per resident lane (the 8-way share of a 1080p frame; measured on C3 at 32 spp, DESIGN.md §3.10: 8-way share 1.007 -> 0.946 ms, 4-way share
     // 1.499 -> 1.548 ms); option "path_prio": waves whose pixels lie in the first path_prio / 256 of
     // a cost-ordered shard run at raised issue priority (0 = off; measured without effect)
     int path_order_pair = 2;
@@ -397,6 +413,7 @@ struct akr_hip_ctx {
             if (e) (void)hipEventDestroy(e);
         if (h_remain) (void)hipHostFree(h_remain);
         if (h_check) (void)hipHostFree(h_check);
+        if (h_miss) (void)hipHostFree(h_miss);
         if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_gather) (void)hipEventDestroy(ev_gather);
@@ -688,6 +705,7 @@ struct akr_hip_ctx {
         d_owork.reserve(kTraceWords);
         d_ocnt.reserve(3);
         d_otmp.reserve(pixel_order_tmp_bytes((uint32_t)std::min<size_t>(n, UINT32_MAX)));
+        if (path_order_pilot_spp > 0) d_pprobe.reserve(n);  // the path pilot's probe (option), ADVICE r4
         cap = n;
     }
 
@@ -757,7 +775,7 @@ struct akr_hip_ctx {
     // decreasing pilot cost (tile order within a cost class).  The pilot traces the camera ray of
     // every slot's first sample with the counting kernel into scratch counters; nothing it does
     // reaches the film, the sampler states or the context's statistics.
-    void pixel_order(uint32_t N, hipStream_t ms) {
+    void pixel_order(uint32_t N, hipStream_t ms, bool count_miss = false) {
         // sized for the capacity by ensure_capacity (the sort's scratch grows with n), so no size
         // query runs per render
         if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
@@ -774,18 +792,42 @@ struct akr_hip_ctx {
         t.step_cap = (uint32_t)path_order_cap;
         // the steps-only build: no hits, no tallies (the counting build spilled and ran ~20 % longer)
         launch_trace(TRACE_PILOT, false, true, true, t, grid_for(TRACE_CLOSEST, n_rays), ms);
+        if (count_miss) {
+            d_miss.reserve(1);
+            HIPCHK(hipMemsetAsync(d_miss.p, 0, sizeof(uint32_t), ms));
+        }
         launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, (uint32_t)(path_order_classes - 1), sub,
-                          d_okey[0].p, d_oidx[0].p, ms);
+                          d_okey[0].p, d_oidx[0].p, ms, count_miss ? d_miss.p : nullptr);
         sort_pixel_order(d_otmp.p, tb, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
         HIPCHK(hipGetLastError());
+    }
+
+    // The miss count of the pilot just issued on `ms` (pixel_order with count_miss), on the host: one
+    // word copied into mapped host memory, the host waiting for the stream (the render's form depends
+    // on it).
+    uint32_t read_pilot_miss(hipStream_t ms) {
+        if (!h_miss) {
+            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_miss), sizeof(uint32_t),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_miss_host), h_miss, 0));
+        }
+        *reinterpret_cast<volatile uint32_t *>(h_miss) = kMappedSentinel;
+        launch_store_word(d_miss.p, d_miss_host, ms);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(ms));
+        const uint32_t m = read_mapped(h_miss);
+        if (m == kMappedSentinel) throw std::runtime_error("pilot: the device never reported its miss count");
+        return m;
     }
 
     // Path pilot: a counting k_path render of S samples per slot (the render's own first samples: a
     // slot's sampler starts from its seed in every render) into the zeroed film, whose probe gives
     // each slot's rays; the film is zeroed again for the render.  Classes of 2^shift rays.
     void pixel_order_path(const PathArgs &base, bool tab, uint32_t grid, uint32_t N, int S, hipStream_t ms) {
-        if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
-        d_pprobe.reserve(N);
+        // S samples trace at most S * (2 max_depth + 1) rays (max(1, max_depth) closest-hit, max_depth shadow)
+        const uint32_t max_rays = (uint32_t)S * (2u * (uint32_t)std::max(base.max_depth, 0) + 1u);
+        if (d_okey[0].n < N || d_oidx[0].n < N || d_pprobe.n < N)
+            throw std::runtime_error("pixel order buffers not sized");
         HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
         PathArgs pp = base;
         pp.spp = (uint32_t)S;
@@ -799,8 +841,8 @@ struct akr_hip_ctx {
         launch_path(true, PATH_PLAIN, tab, pp, std::min<uint32_t>(grid, path_grid[PATH_PLAIN][tab]), ms);
         launch_probe_cost(d_pprobe.p, N, d_okey[1].p, ms);
         HIPCHK(hipMemsetAsync(d_film.p, 0, (size_t)N * sizeof(float4), ms));
-        uint32_t shift = 0;  // at most ~9 rays per sample (max_depth 5: 5 closest-hit + 4 shadow)
-        while (((uint32_t)(9 * S + 1) >> shift) > (uint32_t)path_order_classes) shift++;
+        uint32_t shift = 0;
+        while (((max_rays + 1u) >> shift) > (uint32_t)path_order_classes) shift++;
         launch_order_keys(d_okey[1].p, N, shift, (uint32_t)(path_order_classes - 1), 0, d_okey[0].p, d_oidx[0].p, ms);
         sort_pixel_order(d_otmp.p, d_otmp.n, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
         HIPCHK(hipGetLastError());
@@ -1044,24 +1086,14 @@ struct akr_hip_ctx {
                 pa.probe_clock = probe_clock ? 1u : 0u;
                 pa.spec_depth = (uint32_t)path_spec_depth;
                 pa.spec_alt = path_spec_alt ? 1u : 0u;
-                const bool defer = p.max_depth <= 8 &&
-                                   (path_defer == 1 || (path_defer == 2 && (int64_t)N <= path_defer_pixels &&
-                                                        (int64_t)n_tris() >= path_defer_min_tris));
-                // speculative samples on the lanes a drained queue leaves idle
-                const bool spec = path_spec == 1 || (path_spec == 2 && (int64_t)N <= path_spec_pixels &&
-                                                     (int64_t)n_tris() >= path_defer_min_tris);
-                const int kind = spec ? PATH_SPEC : (defer ? PATH_DEFER : PATH_PLAIN);
                 // the shading's material / light / CDF tables in LDS when they fit
                 const bool tab = path_tab && path_tab_fits(n_mats, n_lights);
-                const uint64_t resident = (uint64_t)path_grid[kind][tab] * (uint64_t)path_grid_pct / 100;
-                const uint32_t grid = (uint32_t)std::max<uint64_t>(
-                    1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
-                pa.min_wait = (uint32_t)(path_min_wait > 0 ? path_min_wait : 40);
-                if (kind == PATH_DEFER) {
-                    d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
-                    pa.contrib = d_contrib.p;
-                    pa.mix = path_mix ? 1u : 0u;
-                }
+                // pixels per resident lane of k_path (the occupancy query's grid)
+                const uint64_t lanes = std::max<uint64_t>(1, (uint64_t)path_grid[PATH_PLAIN][tab] *
+                                                                 (uint64_t)path_grid_pct / 100) * kTraceBlock;
+                const int64_t ppl1000 = (int64_t)((N * 1000 + lanes / 2) / lanes);
+                last_ppl1000 = ppl1000;
+                last_pilot_rays = last_pilot_miss = -1;
                 // the first persistent render of a context runs the pilot once on a few pixels: its
                 // kernels (and rocPRIM's) are loaded then, not inside a later ordered render
                 if (path_order != 0 && !order_warm) {
@@ -1071,18 +1103,56 @@ struct akr_hip_ctx {
                 const int order_min_spp = (int64_t)N <= path_order_share_pixels
                                               ? std::min(path_order_share_min_spp, path_order_min_spp)
                                               : path_order_min_spp;
-                if (path_order != 0 && (kind == PATH_PLAIN || path_order == 2) && p.spp >= order_min_spp && N >= 2) {
-                    if (path_order_pilot_spp > 0)
-                        timed("pilot", ms, [&] { pixel_order_path(pa, tab, grid, (uint32_t)N, path_order_pilot_spp, ms); });
+                pa.min_wait = (uint32_t)(path_min_wait > 0 ? path_min_wait : 40);
+                const bool forced = path_spec == 1 || path_defer != 2;
+                // the pilot can rank pixels for every form (path_order 2), or for k_path only (1)
+                const bool pilot = path_order != 0 && p.spp >= order_min_spp && N >= 2 &&
+                                   (path_order == 2 || (!forced || (path_spec != 1 && path_defer == 0)));
+                const bool path_pilot = pilot && path_order_pilot_spp > 0;
+                // the rule's size and scene tests; its miss test needs the camera-ray pilot
+                const bool size_ok = ppl1000 <= path_tail_ppl10 * 100;
+                const bool tris_ok = path_defer_min_tris == 0 || (int64_t)n_tris() >= path_defer_min_tris;
+                const bool want_miss = !forced && path_order == 2 && pilot && !path_pilot && tris_ok &&
+                                       (path_spec == 2 ? (path_spec_pixels > 0 ? (int64_t)N <= path_spec_pixels : size_ok)
+                                                       : (path_defer_pixels > 0 ? (int64_t)N <= path_defer_pixels : size_ok));
+                if (pilot) {
+                    if (path_pilot)
+                        timed("pilot", ms, [&] { pixel_order_path(pa, tab, std::max<uint32_t>(1, path_grid[PATH_PLAIN][tab]),
+                                                                  (uint32_t)N, path_order_pilot_spp, ms); });
                     else
-                        timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms); });
+                        timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms, want_miss); });
                     pa.order = d_oidx[1].p;
+                }
+                bool tail = false;
+                if (want_miss) {  // the host waits for the pilot's miss count (a few hundred microseconds)
+                    const uint64_t rays = ((uint64_t)N + (1u << path_order_sub) - 1) >> path_order_sub;
+                    const uint32_t miss = read_pilot_miss(ms);
+                    last_pilot_rays = (int64_t)rays;
+                    last_pilot_miss = miss;
+                    tail = (uint64_t)miss * 100 >= (uint64_t)path_tail_miss_pct * rays && miss > 0;
+                }
+                int kind = PATH_PLAIN;
+                if (path_spec == 1) kind = PATH_SPEC;
+                else if (path_defer == 1 && p.max_depth <= 8) kind = PATH_DEFER;
+                else if (path_defer == 2 && tail) kind = path_spec == 2 ? PATH_SPEC : (p.max_depth <= 8 ? PATH_DEFER : PATH_PLAIN);
+                const uint64_t resident = (uint64_t)path_grid[kind][tab] * (uint64_t)path_grid_pct / 100;
+                const uint32_t grid = (uint32_t)std::max<uint64_t>(
+                    1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
+                if (kind == PATH_DEFER) {
+                    d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
+                    pa.contrib = d_contrib.p;
+                    pa.mix = path_mix ? 1u : 0u;
+                }
+                if (pa.order && !(kind == PATH_PLAIN || path_order == 2)) pa.order = nullptr;  // path_order 1
+                if (pa.order) {
+                    const bool small = ppl1000 <= 1500;  // at most 1.5 pixels per resident lane (8-way share)
                     const bool pair = path_order_pair == 3 ||
-                                      (kind != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && N <= 400000)));
+                                      (kind != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && small)));
                     pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
                     // k_path_spec: every wave takes pixels from the whole cost order (FETCH_STRIDE), so
                     // each has cheap pixels whose lanes turn helpers early (option path_spec_fetch)
-                    if (kind == PATH_SPEC && path_spec_fetch >= 0 && (int64_t)N <= path_spec_fetch_pixels)
+                    if (kind == PATH_SPEC && path_spec_fetch >= 0 &&
+                        (path_spec_fetch_pixels > 0 ? (int64_t)N <= path_spec_fetch_pixels : small))
                         pa.order_mode = (uint32_t)path_spec_fetch;
                     pa.prio = (uint32_t)path_prio;
                 }
@@ -1445,6 +1515,7 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_pilot_spp") {
             if (value < 0 || value > 64) throw std::runtime_error("path_order_pilot_spp must be in [0, 64]");
             ctx->path_order_pilot_spp = (int)value;
+            if (value > 0) ctx->cap = 0;  // the next render's ensure_capacity reserves the pilot's probe
         } else if (k == "path_spec_alt") {
             ctx->path_spec_alt = value != 0;
         } else if (k == "path_spec_depth") {
@@ -1456,6 +1527,12 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_spec_fetch") {
             if (value < -1 || value > 3) throw std::runtime_error("path_spec_fetch must be in [-1, 3]");
             ctx->path_spec_fetch = (int)value;
+        } else if (k == "path_tail_ppl10") {
+            if (value < 0) throw std::runtime_error("path_tail_ppl10 must be >= 0");
+            ctx->path_tail_ppl10 = value;
+        } else if (k == "path_tail_miss_pct") {
+            if (value < 0 || value > 100) throw std::runtime_error("path_tail_miss_pct must be in [0, 100]");
+            ctx->path_tail_miss_pct = (int)value;
         } else if (k == "path_spec_pixels") {
             if (value < 0) throw std::runtime_error("path_spec_pixels must be >= 0");
             ctx->path_spec_pixels = value;
@@ -1566,7 +1643,9 @@ namespace {
 // error.  O(n_tris) on `n_threads` threads.
 void check_tris_match_mesh(const akr_hip_ctx *ctx, const akr_bvh_tri *tr, uint64_t n, int n_threads) {
     const uint64_t nt = ctx->n_tris();
-    std::vector<uint8_t> covered(nt, 0);
+    // relaxed atomics: several threads may mark the same triangle (SBVH duplicates), ADVICE r4
+    std::unique_ptr<std::atomic<uint8_t>[]> covered(new std::atomic<uint8_t>[nt]);
+    for (uint64_t g = 0; g < nt; g++) covered[g].store(0, std::memory_order_relaxed);
     const int T = n_threads > 0 ? std::min(n_threads, 64)
                                 : (int)std::min(64u, std::max(1u, std::thread::hardware_concurrency()));
     std::vector<uint64_t> bad(T, UINT64_MAX);
@@ -1589,7 +1668,7 @@ void check_tris_match_mesh(const akr_hip_ctx *ctx, const akr_bvh_tri *tr, uint64
                 bad[t] = r;
                 return;
             }
-            covered[g] = 1;  // racy writes of the same value: fine
+            covered[g].store(1, std::memory_order_relaxed);
         }
     });
     for (uint64_t r : bad)
@@ -1597,7 +1676,7 @@ void check_tris_match_mesh(const akr_hip_ctx *ctx, const akr_bvh_tri *tr, uint64
             throw std::runtime_error("imported BVH: triangle record " + std::to_string(r) + " (gid " +
                                      std::to_string(tr[r].gid) + ") does not match this scene's triangle");
     for (uint64_t g = 0; g < nt; g++)
-        if (!covered[g])
+        if (!covered[g].load(std::memory_order_relaxed))
             throw std::runtime_error("imported BVH: scene triangle " + std::to_string(g) + " is in no leaf");
 }
 
@@ -2135,6 +2214,15 @@ int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered) {
     return guard(ctx, [&] {
         if (form) *form = ctx->last_form;
         if (ordered) *ordered = ctx->last_ordered;
+    });
+}
+
+int akr_hip_render_form_inputs(akr_hip_ctx *ctx, int64_t *pixels_per_lane_x1000, int64_t *pilot_rays,
+                               int64_t *pilot_misses) {
+    return guard(ctx, [&] {
+        if (pixels_per_lane_x1000) *pixels_per_lane_x1000 = ctx->last_ppl1000;
+        if (pilot_rays) *pilot_rays = ctx->last_pilot_rays;
+        if (pilot_misses) *pilot_misses = ctx->last_pilot_miss;
     });
 }
 

@@ -306,6 +306,45 @@ def launch_check(world: int, rank: int):
         dist.destroy_process_group()
 
 
+# Untimed same-run legs of the other BASELINE configs: C2, the reference's Cornell
+# box at 1920x1080, and the C4 stand-in (the synthetic textured hall at 3840x2160).  Each renders a
+# bounded number of spp in the library's form for that scene; the metric's spp (1024 / 256) would add
+# ~2 s each, so they report Msamples/s at a smaller spp and say so.
+SIDE_LEGS = {"cornell": (1920, 1080, 64), "hall": (3840, 2160, 16)}
+
+
+def side_leg(name, device, max_depth, tile, build_kw, stream_of):
+    """Render one side configuration on `device` in a context of its own (scene, BVH, film) and time
+    one render_device call of `spp` samples after a 1-spp warmup.  Returns the leg's record."""
+    import torch
+    from akari_amd import capi, scene
+    W, H, spp = SIDE_LEGS[name]
+    sc = (scene.cornell_scene(ROOT / "tests" / "golden" / "CornellBox-Original.obj.mesh", resolution=(W, H))
+          if name == "cornell" else scene.hall_scene(resolution=(W, H)))
+    cs = scene.compile_scene(sc)
+    dev = torch.device("cuda", device)
+    with capi.HipContext(device) as c:
+        info = scene.upload_scene(c, cs, **build_kw)
+        tiles = capi.rect_array(tile_grid(W, H, tile))
+        film = torch.zeros(W * H * 4, device=dev)
+        rad, wgt = film[:W * H * 3], film[W * H * 3:]
+        st = stream_of(dev)
+        c.render_device(1, max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), st)   # warm (pilot, kernels)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        c.render_device(spp, max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), st)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter() - t
+        form = c.render_form()
+        assert int(wgt.min().item()) == spp and int(wgt.max().item()) == spp
+        return {"workload": {"cornell": "C2 Cornell box (BASELINE.json configs[1])",
+                             "hall": "C4 stand-in: synthetic textured hall (BASELINE.json configs[3])"}[name],
+                "triangles": cs.n_tris, "width": W, "height": H, "spp": spp, "max_depth": max_depth,
+                "Msamples_per_s": round(W * H * spp / t / 1e6, 2), "ms_per_spp": round(t / spp * 1e3, 4),
+                "form": form["form"], "ordered_fetch": form["ordered"], "bvh_nodes": info.n_nodes,
+                "timed": False, "note": f"one render_device of {spp} spp after a 1-spp warmup, untimed leg of this run"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=0,
@@ -360,6 +399,9 @@ def main():
                     help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
     ap.add_argument("--wavefront-spp", type=int, default=16,
                     help="untimed same-run leg in the wavefront form (north_star's layout), spp; 0 = skip")
+    ap.add_argument("--side-legs", type=int, default=1,
+                    help="N = 1, soup: also render C2 (Cornell 1080p, 64 spp) and the C4 stand-in (hall 4K, 16 spp) "
+                         "as untimed legs of the same run (the line's `configs` block); 0 = skip")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearse the N-rank path on a one-GPU box: every rank on device 0, a gloo process group, "
                          "the frame-end gather through host memory; the line says so and is not a measurement")
@@ -654,7 +696,7 @@ def main():
         roofline["latency"] = latency_model(prof, cl, sh, npix, value * 1e6)
     if achieved > HBM_PEAK_GBS:   # the model bytes are not HBM bytes: caches serve most of them
         roofline["note"] = ("the SURVEY.md §8d algorithmic bytes exceed the HBM peak: most node and triangle reads "
-                            "hit L2 or the Infinity Cache (on C3 ~73 % L2 hits by PMC; a small scene's BVH is wholly "
+                            "hit L2 or the Infinity Cache (on C3 ~66 % L2 hits by PMC, profiles/r20g_summary.md; a small scene's BVH is wholly "
                             "cache-resident), so frac is a model figure; hbm_frac is the HBM traffic measured by PMC "
                             "over the same launch time")
     if iso and "trace_shadow" in iso:   # the shadow trace alone: its own roofline (wavefront form)
@@ -688,6 +730,15 @@ def main():
                          f"{args.cpu_spp} spp, same scene and BVH, reference intersectAABB, {dt:.1f} s",
                "value_tight_cull": round(cpx * args.cpu_spp / dt_tight / 1e6, 4)}
 
+    configs = None
+    if args.side_legs and world == 1 and args.scene == "soup":
+        side_kw = dict(build_kw)
+        configs = {}
+        for name in SIDE_LEGS:
+            configs[name] = side_leg(name, local, args.max_depth, args.tile, side_kw,
+                                     lambda d: torch.cuda.current_stream(d).cuda_stream)
+            log(f"[rank 0] side leg {name}: {configs[name]}")
+
     line = {
         "metric": {"soup": METRIC, "cornell": METRIC_CORNELL, "hall": METRIC_HALL}[args.scene], "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": K, "warmup": Wm,
         "ms_per_step": round(elapsed / K * 1e3, 3), "ms_per_spp": round(elapsed / spp * 1e3, 4),
@@ -699,6 +750,7 @@ def main():
         "wavefront_ms_per_spp": wavefront["ms_per_spp"] if wavefront else None,
         "wavefront": wavefront,
         "roofline": roofline, "cpu_baseline": cpu, "frame_check": frame_check,
+        "configs": configs,
         # per-kernel averages from an untimed pass with events on every launch (the timed region
         # times trace_closest only: events around every launch cost ~7 % at an 8-way rank)
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}

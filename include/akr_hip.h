@@ -212,10 +212,16 @@ const char *akr_hip_last_error(const akr_hip_ctx *ctx);
  * "lookahead" (speculative sample lanes per pixel, DESIGN.md §3.7: 1 = off (default), 0 = on
  * whenever "slot_target" gives a pixel two or more lanes, 2..64 = on with at most that many lanes;
  * results are identical for every value), "slot_target" (lookahead path slots per pass).
- * Render forms and their tuning (all give the same bits, DESIGN.md §3.8-3.10): "path" (0 wavefront,
- * 1 persistent kernel, 2 auto), "path_defer", "path_defer_pixels", "path_defer_min_tris", "path_auto_pixels",
- * "path_auto_complex", "path_tab", "path_mix", "path_order", "path_order_min_spp",
- * "path_order_share_pixels", "path_order_share_min_spp", "path_order_shift", "path_order_pair", "path_prio", "path_min_wait", "path_grid_pct".
+ * Render forms and their tuning (all give the same bits, DESIGN.md §3.8-3.12): "path" (0 wavefront,
+ * 1 persistent kernel, 2 auto), "path_auto_pixels", "path_auto_complex";
+ * the persistent form: "path_spec" (k_path_spec: 1 always, 0 never, 2 auto), "path_defer" (k_path_defer:
+ * 1 forced, 0 k_path forced, 2 auto), the auto rule's "path_tail_ppl10" and "path_tail_miss_pct" and its
+ * overrides "path_spec_pixels", "path_defer_pixels", "path_defer_min_tris"; k_path_spec's "path_spec_depth",
+ * "path_spec_alt", "path_spec_fetch", "path_spec_fetch_pixels";
+ * "path_tab", "path_mix", "path_min_wait", "path_grid_pct", "path_prio";
+ * the cost order: "path_order", "path_order_min_spp", "path_order_share_pixels", "path_order_share_min_spp",
+ * "path_order_shift", "path_order_pair", "path_order_classes", "path_order_cap", "path_order_sub",
+ * "path_order_pilot_spp", "wave_order" (the wavefront's camera rays in cost order).
  * "verify" (default 1): in-band film check after every render.  Test only: "pixel_probe" (record
  * akr_pixel_probe per slot), "fault_test" (raise the hang guard's fault word once), "ray_steps",
  * "serial_shadow", "any_far_first", "la_early_exit". */
@@ -326,6 +332,11 @@ int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
 #define AKR_FORM_PATH_DEFER 3
 #define AKR_FORM_PATH_SPEC 4
 int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered);
+/* The inputs of the last persistent render's form choice: its pixels per resident
+ * lane x 1000, and the pilot's camera rays and how many of them missed the scene (-1 when the choice
+ * did not read the pilot: a forced form, no pilot, or a render too large for a tail form). */
+int akr_hip_render_form_inputs(akr_hip_ctx *ctx, int64_t *pixels_per_lane_x1000, int64_t *pilot_rays,
+                               int64_t *pilot_misses);
 int akr_hip_synchronize(akr_hip_ctx *ctx);
 /* Copies the first n records of the last render's pixel probe (see akr_pixel_probe); fails when
  * the last render ran without option "pixel_probe" or has fewer slots. */

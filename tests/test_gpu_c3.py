@@ -253,3 +253,25 @@ def test_c3_lit_view_render_bit_exact(c3):
     finally:
         c = cs.camera
         ctx.set_camera(c.position, c.rotation, c.fov, c.resolution)
+
+
+def test_c3_8way_share_takes_k_path_spec(c3):
+    """The form rule on the headline scene: an 8-way share of the 1080p frame (64x64
+    tiles, as the bench) at 16 spp under the default options runs k_path_spec in cost order — about
+    one pixel per resident lane, and the pilot finds the background (camera rays that miss the soup) —
+    and equals the oracle bit for bit.  The Cornell box's share takes k_path (test_gpu_cornell1080)."""
+    ctx, cs, orc, _ = c3
+    share = dist.tiles_for_rank(W, H, 64, 0, 8)
+    for k, v in dict(path=2, path_defer=2, path_spec=2, path_order=2, path_order_min_spp=16).items():
+        ctx.set_option(k, v)
+    try:
+        rad, w = ctx.render(16, 5, share, W, H)
+        form, inp = ctx.render_form(), ctx.render_form_inputs()
+    finally:
+        for k, v in DEFAULTS.items():
+            ctx.set_option(k, v)
+    assert form == {"form": "k_path_spec", "ordered": True}, (form, inp)
+    assert 0.5 < inp["pixels_per_lane"] < 1.5 and inp["pilot_misses"] > 0.2 * inp["pilot_rays"], inp
+    orad, ow, _ = orc.render(16, 5, tiles=share, n_threads=16)
+    assert np.array_equal(w, ow)
+    assert np.array_equal(rad, orad), f"radiance differs (max abs diff {np.abs(rad - orad).max()})"

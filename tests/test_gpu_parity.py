@@ -604,6 +604,7 @@ def test_spec_and_order_options_are_validated(hip_ctx_factory):
     with hip_ctx_factory(0) as ctx:
         for key, good, bad in (("path_spec_depth", (1, 3), (0, 4)), ("path_spec_fetch", (-1, 3), (-2, 5)),
                                ("path_order_pilot_spp", (0, 64), (-1, 65)), ("path_spec_fetch_pixels", (0, 1 << 40), (-1,)),
+                               ("path_tail_ppl10", (0, 1 << 40), (-1,)), ("path_tail_miss_pct", (0, 100), (-1, 101)),
                                ("wave_order", (0, 1), ()), ("path_spec_alt", (0, 1), ())):
             for v in good:
                 ctx.set_option(key, v)
@@ -629,29 +630,59 @@ def test_auto_form_by_shading(hip_ctx_factory):
                 _check_render(ctx, orc, 3, 5, [(0, 0, 32, 32)], 32, 32)
                 want = "path" if (simple or complex_ok) else "trace_closest"
                 assert set(ctx.kernel_stats()) == {want}, (sc, complex_ok, ctx.kernel_stats())
-                # a 36-triangle scene takes k_path even at a small pixel count (path_defer_min_tris)
+                # 3 spp: no pilot, so the constant-shading scene takes k_path
                 assert ctx.render_form()["form"] == ("k_path" if (simple or complex_ok) else "wavefront")
-    with hip_ctx_factory(0) as ctx:   # >= 10K triangles at <= 1.2 M pixels: the speculative form
+    # the persistent form by the pilot rule: a tail form (k_path_spec, or
+    # k_path_defer with path_spec 0) for a render of few pixels per resident lane whose pilot camera
+    # rays miss the scene often enough; k_path otherwise, and without a pilot
+    with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
-        _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
-        assert ctx.render_form() == {"form": "k_path_spec", "ordered": False}
-        ctx.set_option("path_spec", 0)    # without it, the deferred form (<= 600K pixels)
-        _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
-        assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
-        # the cost-ordered fetch from path_order_min_spp (16) samples
-        _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
+        tiles = [(0, 0, 48, 27)]
+        _check_render(ctx, orc, 3, 5, tiles, 48, 27)     # below the order's 16-spp floor: no pilot
+        assert ctx.render_form() == {"form": "k_path", "ordered": False}
+        assert ctx.render_form_inputs()["pilot_misses"] == -1
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
+        inp = ctx.render_form_inputs()
+        assert inp["pilot_rays"] == 48 * 27 and 0.15 * 48 * 27 <= inp["pilot_misses"] < 48 * 27, inp
+        assert 0 < inp["pixels_per_lane"] < 0.01
+        assert ctx.render_form() == {"form": "k_path_spec", "ordered": True}
+        ctx.set_option("path_spec", 0)    # the rule's tail form is then the deferred one
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}
-        # a render of at most path_order_share_pixels pixels takes it from path_order_share_min_spp
-        # (16) samples even when the general floor is higher
-        ctx.set_option("path_order_min_spp", 64)
-        _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
-        assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}
-        ctx.set_option("path_order_share_pixels", 1000)
-        _check_render(ctx, orc, 16, 5, [(0, 0, 48, 27)], 48, 27)
-        assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
-        ctx.set_option("path_defer_min_tris", 10 ** 9)
-        _check_render(ctx, orc, 3, 5, [(0, 0, 48, 27)], 48, 27)
+        ctx.set_option("path_spec", 2)
+        ctx.set_option("path_tail_miss_pct", 100)   # too few misses: k_path
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
+        assert ctx.render_form() == {"form": "k_path", "ordered": True}
+        ctx.set_option("path_tail_miss_pct", 15)
+        ctx.set_option("path_tail_ppl10", 0)        # too many pixels per lane: k_path, the pilot not read
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
+        assert ctx.render_form() == {"form": "k_path", "ordered": True}
+        assert ctx.render_form_inputs()["pilot_misses"] == -1
+        ctx.set_option("path_tail_ppl10", 60)
+        ctx.set_option("path_spec_pixels", 1000)    # the explicit size override (1296 pixels > 1000)
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         assert ctx.render_form()["form"] == "k_path"
+        ctx.set_option("path_spec_pixels", 0)
+        ctx.set_option("path_defer_min_tris", 10 ** 9)
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
+        assert ctx.render_form()["form"] == "k_path"
+        ctx.set_option("path_defer_min_tris", 0)
+        # a render of at most path_order_share_pixels pixels takes the order from path_order_share_min_spp
+        # (16) samples even when the general floor is higher; without the order, no tail form
+        ctx.set_option("path_order_min_spp", 64)
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
+        assert ctx.render_form() == {"form": "k_path_spec", "ordered": True}
+        ctx.set_option("path_order_share_pixels", 1000)
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
+        assert ctx.render_form() == {"form": "k_path", "ordered": False}
+        # forced forms ignore the rule
+        ctx.set_option("path_spec", 1)
+        _check_render(ctx, orc, 3, 5, tiles, 48, 27)
+        assert ctx.render_form() == {"form": "k_path_spec", "ordered": False}
+        ctx.set_option("path_spec", 2)
+        ctx.set_option("path_defer", 1)
+        _check_render(ctx, orc, 3, 5, tiles, 48, 27)
+        assert ctx.render_form() == {"form": "k_path_defer", "ordered": False}
 
 
 def _tab_fits(cs):

@@ -7,30 +7,39 @@
 #   sq     wave-time split (WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY) + VALU issue
 #   lat    VmemLatency (SQ_INST_LEVEL_VMEM accumulated / SQ_INSTS_VMEM), VMEM reads, TCP->TCC read latency
 #   ea     L2 -> fabric read requests in flight (TCC_EA0_RDREQ_LEVEL) and their count: fabric latency
+#   rq     L2 -> fabric read requests by size (32 / 64 / 128 B): with tools/fetch_calib's calibration
+#          (profiles/*_fetch_calib.json) these give the read bytes without FETCH_SIZE's blanket factor
+#   rq2    128-B requests as FETCH_SIZE counts them (TCC_BUBBLE), DRAM-bound requests, L2 hits / misses
 # tools/prof_summary.py <tag> turns gpurun_out/prof_<tag>/ into profiles/<tag>_{summary.md,traffic.json}.
-# Usage (GPU box, repo root): tools/profile_driver.sh <tag> [bench args]
+# Usage (GPU box, repo root): [PASSES="rq rq2"] tools/profile_driver.sh <tag> [bench args]
 tag=${1:-drv}; shift
 args=${*:-"--steps 20 --warmup 5"}
+passes=${PASSES:-"kt fetch write tcc sq lat ea rq rq2"}
 export TMPDIR=/tmp
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
 echo "$args" > "$out/args.txt"
-run() {  # name, rocprofv3 options...
-    local name=$1; shift
-    echo "pass $name: $*" | tee -a "$out/progress.txt"
-    timeout -k 10 300 rocprofv3 "$@" --kernel-trace --output-format csv -d "$out/$name" -o run -- \
-        python3 bench.py $args --cpu-baseline 0 > "$out/$name.log" 2>&1
-    local rc=$?
+declare -A PMC=(
+    [fetch]="FETCH_SIZE"
+    [write]="WRITE_SIZE"
+    [tcc]="TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum"
+    [sq]="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+    [lat]="VmemLatency SQ_INSTS_VMEM_RD TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum"
+    [ea]="TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"
+    [rq]="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+    [rq2]="TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum TCC_MISS_sum TCC_HIT_sum"
+)
+for name in $passes; do
+    echo "pass $name" | tee -a "$out/progress.txt"
+    if [ "$name" = kt ]; then
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- \
+            python3 bench.py $args > "$out/kt.log" 2>&1
+    else
+        timeout -s KILL 240 rocprofv3 --pmc ${PMC[$name]} --kernel-trace --output-format csv -d "$out/$name" -o run -- \
+            python3 bench.py $args --cpu-baseline 0 > "$out/$name.log" 2>&1
+    fi
+    rc=$?
     echo "pass $name rc=$rc" | tee -a "$out/progress.txt"
-    return $rc
-}
-echo "pass kt" | tee -a "$out/progress.txt"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- \
-    python3 bench.py $args > "$out/kt.log" 2>&1 || exit $?
-run fetch --pmc FETCH_SIZE &&
-run write --pmc WRITE_SIZE &&
-run tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum &&
-run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE &&
-run lat --pmc VmemLatency SQ_INSTS_VMEM_RD TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum &&
-run ea --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum &&
+    [ $rc -eq 0 ] || exit $rc
+done
 echo "profile $tag done"
