@@ -483,10 +483,11 @@ class HipContext:
 
     def path_profile(self) -> dict:
         """k_path phase profile of the counted launches since reset_stats (ticks: 100 MHz)."""
-        out = (C.c_uint64 * 13)()
-        self._check(self.lib.akr_hip_path_profile(self.h, out, 13))
         keys = ("waves", "outer", "procs", "trav_iters", "t_proc", "t_trav", "t_leaf", "t_total", "t_max", "lanes_proc",
-                "t_shade", "spec_started", "spec_aborted")
+                "t_shade", "spec_started", "spec_aborted", "tv_issue", "tv_wait", "tv_comp", "tl_issue", "tl_wait",
+                "tl_comp")
+        out = (C.c_uint64 * len(keys))()
+        self._check(self.lib.akr_hip_path_profile(self.h, out, len(keys)))
         return dict(zip(keys, (int(v) for v in out)))
 
     def trace_counts(self) -> dict:

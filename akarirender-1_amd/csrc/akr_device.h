@@ -280,6 +280,9 @@ struct PathProfile {
     unsigned long long lanes_proc; // waiting lanes processed, summed over phases
     unsigned long long t_shade;    // ticks of A spent on finished rays' results (shading, shadow hand-over)
     unsigned long long spec_started, spec_aborted;  // k_path_spec: speculative samples started / dropped
+    // time split of B and C (ticks, wave-uniform clocks summed per wave): load issue, the explicit
+    // wait for the loads, the dependent work after them
+    unsigned long long tv_issue, tv_wait, tv_comp, tl_issue, tl_wait, tl_comp;
 };
 
 // Persistent path kernel (k_path): the whole sample loop of every pixel of the tile list.

@@ -308,19 +308,30 @@ __device__ __forceinline__ int visit_wide(const float4 *wn, uint32_t &cur, V3 o,
 // origins and steps are <= 2^40, which bounds every term below 2^126 (no overflow, no NaN); with
 // tmin >= 0 the reference's "t < 0" reject cannot fire and TIGHT's t <= m1 implies m0 <= m1, and
 // t < tmax is t <= tmaxp (the float below tmax).
-template <bool ANY>
-__device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, V3 o, uint32_t dpos, V3 invd, float tmin,
-                                               float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
-                                               uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
-    // a 32-bit byte offset from the array base (SGPR base + VGPR offset addressing: one 32-bit shift
-    // instead of two 64-bit address operations per visit, 0.7 % of the frame); the wide view holds
-    // fewer than 2^26 nodes (checked when it is uploaded, kMaxWideNodes)
+// The wide node's four 16-B loads (a 32-bit byte offset from the array base: SGPR base + VGPR offset
+// addressing, one 32-bit shift instead of two 64-bit address operations per visit, 0.7 % of the
+// frame; the wide view holds fewer than 2^26 nodes, checked when it is uploaded, kMaxWideNodes)
+struct WideNode {
+    float4 h;
+    uint4 c, qa, qb;
+};
+__device__ __forceinline__ WideNode wide_load(const float4 *wn, uint32_t cur) {
     const char *wb = reinterpret_cast<const char *>(wn);
     const uint32_t off = cur << 6;
-    const float4 h = *reinterpret_cast<const float4 *>(wb + off);
-    const uint4 c = *reinterpret_cast<const uint4 *>(wb + off + 16);
-    const uint4 qa = *reinterpret_cast<const uint4 *>(wb + off + 32);
-    const uint4 qb = *reinterpret_cast<const uint4 *>(wb + off + 48);
+    WideNode nd;
+    nd.h = *reinterpret_cast<const float4 *>(wb + off);
+    nd.c = *reinterpret_cast<const uint4 *>(wb + off + 16);
+    nd.qa = *reinterpret_cast<const uint4 *>(wb + off + 32);
+    nd.qb = *reinterpret_cast<const uint4 *>(wb + off + 48);
+    return nd;
+}
+
+template <bool ANY>
+__device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t &cur, V3 o, uint32_t dpos, V3 invd,
+                                                    float tmin, float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
+                                                    uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
+    const float4 h = nd.h;
+    const uint4 c = nd.c, qa = nd.qa, qb = nd.qb;
     uint32_t meta = __float_as_uint(h.w);
 #ifdef AKR_PROBE_EXTRA_VALU  // bottleneck probe only: ~AKR_PROBE_EXTRA_VALU dependent VALU ops per visit
     {
@@ -367,6 +378,14 @@ __device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, 
     wide_order_push<ANY>(qb.z, qb.w, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid,
                          sp);
     return tested;
+}
+
+template <bool ANY>
+__device__ __forceinline__ int visit_wide_lean(const float4 *wn, uint32_t &cur, V3 o, uint32_t dpos, V3 invd, float tmin,
+                                               float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
+                                               uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
+    const WideNode nd = wide_load(wn, cur);
+    return visit_wide_lean_node<ANY>(nd, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, ovf, ovf_threads, tid, gtid, sp);
 }
 
 // The float just below `x` (x not NaN): t < x  <=>  t <= below(x) for every float t.
@@ -1460,6 +1479,10 @@ struct PathCount {
     unsigned long long rays[2] = {0, 0}, box[2] = {0, 0}, tri[2] = {0, 0}, visit[2] = {0, 0}, deep[2] = {0, 0},
                        leaf[2] = {0, 0};
     unsigned long long strav = 0, sleaf = 0, stri = 0, iters = 0;
+    // time split of the traversal (v) and leaf (l) phases, wave ticks: issuing the node / leaf
+    // loads, waiting for them (an explicit vmcnt(0) wait between two clock reads), the dependent
+    // work after they return (slot tests, stack, ballots; leaf box and triangle loop)
+    unsigned long long tv_issue = 0, tv_wait = 0, tv_comp = 0, tl_issue = 0, tl_wait = 0, tl_comp = 0;
     bool deep_now = false;
 };
 
@@ -1469,73 +1492,148 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
                                               glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
                                               PathCount &c) {
     while (true) {
-        if (COUNT) {
+        [[maybe_unused]] unsigned long long tc = 0;
+        if constexpr (COUNT) {
             c.strav++;
             c.sleaf += busy ? 1 : 0;
             c.iters++;
-        }
-        if (busy && is_internal(r.cur)) {
-            const int nt = visit_wide_lean<false>(wn, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf,
-                                                  ovf_threads, tid, gtid, r.sp);
-            if (COUNT) {
+            // the counting build splits the iteration's time: issue, wait, work
+            const bool vis = busy && is_internal(r.cur);
+            const unsigned long long ta = wall_clock64();
+            WideNode nd{};
+            if (vis) nd = wide_load(wn, r.cur);
+            const unsigned long long tb = wall_clock64();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tc = wall_clock64();
+            c.tv_issue += tb - ta;
+            c.tv_wait += tc - tb;
+            if (vis) {
+                const int nt = visit_wide_lean_node<false>(nd, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack,
+                                                           ovf, ovf_threads, tid, gtid, r.sp);
                 c.box[kind] += nt;
                 c.visit[kind]++;
                 c.deep_now = c.deep_now || r.sp > kStackLds;
             }
+        } else if (busy && is_internal(r.cur)) {
+            visit_wide_lean<false>(wn, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf, ovf_threads, tid,
+                                   gtid, r.sp);
         }
         if (busy && r.leaf == AKR_CHILD_EMPTY && is_leaf(r.cur)) {
             r.leaf = r.cur;  // postpone the leaf and keep descending
             r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
         }
         const unsigned long long searching = __ballot(busy && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
-        if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
-            (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0))
+        if constexpr (COUNT) {
+            const bool stop = (uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+                              (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0);
+            c.tv_comp += wall_clock64() - tc;
+            if (stop) break;
+        } else if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+                   (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0)) {
             break;
+        }
     }
 }
 
-// C. the leaf phase: the pending leaf's exact box with the current best, then its triangles;
-// returns true when an occlusion ray (kind 1) found its first hit
+// The counting build's leaf tests: the leaf's exact box with the current best, then its triangles
+// (the header, the first and the second triangle's records already loaded)
 template <bool COUNT>
-__device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const float4 *wide_leaves, PathCount &c) {
+__device__ __forceinline__ bool leaf_tests(int kind, PathRay &r, const float4 *lr, float4 l0, float4 l1, float4 pa0,
+                                           float4 pb0, float4 pc0, float4 pa1, float4 pb1, float4 pc1, PathCount &c) {
     bool hit_any = false;
-    if (busy && r.leaf != AKR_CHILD_EMPTY) {
-        const float4 *lr = wide_leaves + (r.leaf & 0x7FFFFFFFu);
-        const float4 l0 = lr[0], l1 = lr[1];
-        const float4 pa0 = lr[2], pb0 = lr[3], pc0 = lr[4];
-        // the second triangle's record is fetched with the header as well (one dependent round trip
-        // less for leaves of two or more triangles; whole frame 5.00 -> 4.86 ms per spp,
-        // profiles/r18_leaf_pf2_ab.log); the blob is padded, so this never reads past its end
-        const float4 pa1 = lr[5], pb1 = lr[6], pc1 = lr[7];
-        const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, r.o, r.invd, r.tmin, r.tmax);
-        const bool in = !(tl < 0.0f || tl > r.best);
-        if (COUNT) {
-            c.box[kind]++;
-            c.leaf[kind]++;
-        }
-        const uint32_t cnt = in ? fbits(l1.w) : 0u;
-        const float4 *tp = lr + 2;
-        for (uint32_t k = 0; k < cnt; k++) {
-            if (COUNT && lane_prefix(__ballot(1)) == 0) c.stri += 64;
-            const float4 ta = k == 0 ? pa0 : (k == 1 ? pa1 : tp[3 * k + 0]);
-            const float4 tb = k == 0 ? pb0 : (k == 1 ? pb1 : tp[3 * k + 1]);
-            const float4 tc = k == 0 ? pc0 : (k == 1 ? pc1 : tp[3 * k + 2]);
-            if (COUNT) c.tri[kind]++;
-            float t, u, v;
-            if (mt(r.o, r.d, r.tmin, r.tmax, ta, tb, tc, r.best, t, u, v)) {
-                r.best = t;
-                r.bu = u;
-                r.bv = v;
-                r.bgid = fbits(ta.w);
-                if (kind) {
-                    hit_any = true;
-                    break;
-                }
+    const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, r.o, r.invd, r.tmin, r.tmax);
+    const bool in = !(tl < 0.0f || tl > r.best);
+    if (COUNT) {
+        c.box[kind]++;
+        c.leaf[kind]++;
+    }
+    const uint32_t cnt = in ? fbits(l1.w) : 0u;
+    const float4 *tp = lr + 2;
+    for (uint32_t k = 0; k < cnt; k++) {
+        if (COUNT && lane_prefix(__ballot(1)) == 0) c.stri += 64;
+        const float4 ta = k == 0 ? pa0 : (k == 1 ? pa1 : tp[3 * k + 0]);
+        const float4 tb = k == 0 ? pb0 : (k == 1 ? pb1 : tp[3 * k + 1]);
+        const float4 tc = k == 0 ? pc0 : (k == 1 ? pc1 : tp[3 * k + 2]);
+        if (COUNT) c.tri[kind]++;
+        float t, u, v;
+        if (mt(r.o, r.d, r.tmin, r.tmax, ta, tb, tc, r.best, t, u, v)) {
+            r.best = t;
+            r.bu = u;
+            r.bv = v;
+            r.bgid = fbits(ta.w);
+            if (kind) {
+                hit_any = true;
+                break;
             }
         }
-        r.leaf = AKR_CHILD_EMPTY;
     }
+    r.leaf = AKR_CHILD_EMPTY;
     return hit_any;
+}
+
+// C. the leaf phase: the pending leaf's exact box with the current best, then its triangles;
+// returns true when an occlusion ray (kind 1) found its first hit.  The leaf's header and its first
+// two triangle records are one batch of eight 16-B loads: one dependent round trip less for leaves of
+// two or more triangles (whole frame 5.00 -> 4.86 ms per spp, profiles/r18_leaf_pf2_ab.log); the blob
+// is padded, so this never reads past its end.
+template <bool COUNT>
+__device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const float4 *wide_leaves, PathCount &c) {
+    if constexpr (!COUNT) {  // (the loads and tests written out here: through leaf_tests the compiler
+                             // allocates the persistent kernels' registers differently)
+        bool hit_any = false;
+        if (busy && r.leaf != AKR_CHILD_EMPTY) {
+            const float4 *lr = wide_leaves + (r.leaf & 0x7FFFFFFFu);
+            const float4 l0 = lr[0], l1 = lr[1];
+            const float4 pa0 = lr[2], pb0 = lr[3], pc0 = lr[4];
+            const float4 pa1 = lr[5], pb1 = lr[6], pc1 = lr[7];
+            const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, r.o, r.invd, r.tmin, r.tmax);
+            const bool in = !(tl < 0.0f || tl > r.best);
+            const uint32_t cnt = in ? fbits(l1.w) : 0u;
+            const float4 *tp = lr + 2;
+            for (uint32_t k = 0; k < cnt; k++) {
+                const float4 ta = k == 0 ? pa0 : (k == 1 ? pa1 : tp[3 * k + 0]);
+                const float4 tb = k == 0 ? pb0 : (k == 1 ? pb1 : tp[3 * k + 1]);
+                const float4 tc = k == 0 ? pc0 : (k == 1 ? pc1 : tp[3 * k + 2]);
+                float t, u, v;
+                if (mt(r.o, r.d, r.tmin, r.tmax, ta, tb, tc, r.best, t, u, v)) {
+                    r.best = t;
+                    r.bu = u;
+                    r.bv = v;
+                    r.bgid = fbits(ta.w);
+                    if (kind) {
+                        hit_any = true;
+                        break;
+                    }
+                }
+            }
+            r.leaf = AKR_CHILD_EMPTY;
+        }
+        return hit_any;
+    } else {  // the counting build splits the phase's time: issue, wait, tests
+        bool hit_any = false;
+        const unsigned long long ta = wall_clock64();
+        const bool in_leaf = busy && r.leaf != AKR_CHILD_EMPTY;
+        const float4 *lr = wide_leaves + (r.leaf & 0x7FFFFFFFu);
+        float4 l0{}, l1{}, pa0{}, pb0{}, pc0{}, pa1{}, pb1{}, pc1{};
+        if (in_leaf) {
+            l0 = lr[0];
+            l1 = lr[1];
+            pa0 = lr[2];
+            pb0 = lr[3];
+            pc0 = lr[4];
+            pa1 = lr[5];
+            pb1 = lr[6];
+            pc1 = lr[7];
+        }
+        const unsigned long long tb = wall_clock64();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long tc = wall_clock64();
+        if (in_leaf) hit_any = leaf_tests<true>(kind, r, lr, l0, l1, pa0, pb0, pc0, pa1, pb1, pc1, c);
+        c.tl_issue += tb - ta;
+        c.tl_wait += tc - tb;
+        c.tl_comp += wall_clock64() - tc;
+        return hit_any;
+    }
 }
 
 // A fresh ray into the traversal state: lean rays enter the loop (returns true: the lane is busy),
@@ -1685,6 +1783,12 @@ __device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &
         atomicMax(&q.t_max, tot);
         atomicAdd(&q.lanes_proc, p_lanes);
         atomicAdd(&q.t_shade, p_tsh);
+        atomicAdd(&q.tv_issue, c.tv_issue);
+        atomicAdd(&q.tv_wait, c.tv_wait);
+        atomicAdd(&q.tv_comp, c.tv_comp);
+        atomicAdd(&q.tl_issue, c.tl_issue);
+        atomicAdd(&q.tl_wait, c.tl_wait);
+        atomicAdd(&q.tl_comp, c.tl_comp);
     }
     const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
     for (int m = 0; m < 2; m++) {

@@ -55,7 +55,8 @@ def log(*a):
 def measured_traffic(kernel, workload, spp=None, profiles_dir=None):
     """The PMC record of `kernel` from the newest committed profile of this exact workload
     (profiles/<tag>_traffic.json, written by tools/prof_summary.py from separate rocprofv3 passes of
-    tools/profile_driver.sh, gfx950 FETCH_SIZE x2 correction).  A profile matches only when its
+    tools/profile_driver.sh: read bytes from the fabric request counts by size, calibrated by
+    tools/fetch_calib.hip, profiles/r21_fetch_calib.json).  A profile matches only when its
     workload equals the line's `config` field for field, so a 1-spp, unordered or whole-frame
     profile never stands in for a 1040-spp ordered launch or a rank's share.  PMC passes cannot run
     inside the timed region, so the figures are the profile's.  Returns (record, source) with
@@ -76,12 +77,16 @@ def measured_traffic(kernel, workload, spp=None, profiles_dir=None):
             if "hbm_bytes_per_spp" not in rec:
                 continue
             rec["traffic"] = rec["hbm_bytes_per_spp"] * spp
+            if "read_bytes_per_spp" in rec:
+                rec["read_traffic"] = rec["read_bytes_per_spp"] * spp
             if "l2_req_bytes_per_spp" in rec:
                 rec["l2_bytes"] = rec["l2_req_bytes_per_spp"] * spp
         else:
             if "hbm_bytes_per_launch" not in rec:
                 continue
             rec["traffic"] = rec["hbm_bytes_per_launch"]
+            if "read_bytes" in rec:
+                rec["read_traffic"] = rec["read_bytes"]
             if "l2_req_bytes_per_launch" in rec:
                 rec["l2_bytes"] = rec["l2_req_bytes_per_launch"]
         best = (rec, f"profiles/{p.name}")
@@ -119,6 +124,34 @@ def latency_model(prof, cl, sh, npix, samples_per_s):
                             "issue_stalled": round(c["SQ_WAIT_INST_ANY"] / wc, 4),
                             "issuing": round(c["SQ_ACTIVE_INST_ANY"] / wc, 4),
                             "valu_active": round(c["SQ_ACTIVE_INST_VALU"] / wc, 4)}
+    return out
+
+
+def time_split(pp, counts):
+    """Where the persistent kernel's wave time goes, from the counting build's
+    wave-uniform clocks over the untimed 1-spp counting pass (kernels.hip path_traverse / path_leaf):
+    processing phases (shading among them), the traversal phase split into issuing the wide node's
+    loads, waiting for them and the dependent work after them (slot tests, stack, ballots), the leaf
+    phase split the same way (waiting for the header + two triangles; box and triangle tests), and the
+    rest (loop control, the pixel fetch).  Fractions of the summed wave lifetimes; the lane factors
+    (busy lanes per traversal slot, triangle tests per triangle-loop slot) say how much of a busy
+    wave's issue does useful work."""
+    tot = pp.get("t_total", 0)
+    if not tot:
+        return None
+    f = lambda x: round(x / tot, 4)
+    cl = counts["per_mode"]["closest"]
+    sh = counts["per_mode"]["shadow"]
+    out = {"processing": f(pp["t_proc"]), "shading": f(pp["t_shade"]),
+           "traversal": {"total": f(pp["t_trav"]), "issue": f(pp["tv_issue"]), "wait": f(pp["tv_wait"]),
+                         "work": f(pp["tv_comp"])},
+           "leaf": {"total": f(pp["t_leaf"]), "issue": f(pp["tl_issue"]), "wait": f(pp["tl_wait"]), "work": f(pp["tl_comp"])},
+           "other": f(tot - pp["t_proc"] - pp["t_trav"] - pp["t_leaf"]),
+           "lanes": {"traversal_busy": round((cl["visits"] + sh["visits"]) / max(1, cl["slots_traversal"]), 4),
+                     "triangle_loop": round((cl["tri_tests"] + sh["tri_tests"]) / max(1, cl["slots_tri"]), 4)},
+           "iterations_per_wave": round(pp["trav_iters"] / max(1, pp["waves"]), 1),
+           "source": "counting build, untimed 1-spp pass; wave-uniform wall clocks (100 MHz) around an explicit "
+                     "vmcnt(0) wait after each node / leaf load batch"}
     return out
 
 
@@ -525,6 +558,7 @@ def main():
     torch.cuda.synchronize(dev)
     counts = ctx.trace_counts()
     cstats = ctx.kernel_stats()
+    pprof = ctx.path_profile()   # the counting build's phase clocks (persistent forms only)
     ctx.set_option("count_tests", 0)
     ctx.reset_stats()
     # events around every launch cost nothing on a whole frame but ~6 % of an 8-way rank's step;
@@ -661,12 +695,21 @@ def main():
     traffic = prof["traffic"] if prof else None
     # hardware fraction beside the model one: the PMC-measured HBM bytes over the live launch time
     hbm_achieved = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
+    # read-only HBM fraction (north_star: "HBM-read roofline"): the L2 -> fabric read bytes, from the
+    # request counts by size, calibrated on the traversal's widths (profiles/r21_fetch_calib.json: every
+    # request is 128 B); Infinity-Cache hits are inside it, so it bounds the HBM reads from above
+    read_traffic = prof.get("read_traffic") if prof else None
+    hbm_read_achieved = read_traffic / (avg_ms * 1e-3) / 1e9 if read_traffic else None
     l2_bytes = prof.get("l2_bytes") if prof else None
     l2_achieved = l2_bytes / (avg_ms * 1e-3) / 1e9 if l2_bytes else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "hbm_achieved": round(hbm_achieved, 1) if hbm_achieved else None,
                 "hbm_frac": round(hbm_achieved / HBM_PEAK_GBS, 4) if hbm_achieved else None,
+                "hbm_read_achieved": round(hbm_read_achieved, 1) if hbm_read_achieved else None,
+                "hbm_read_frac": round(hbm_read_achieved / HBM_PEAK_GBS, 4) if hbm_read_achieved else None,
+                "read_bytes_source": prof.get("read_bytes_source") if prof else None,
+                "fetch_calibration": "profiles/r21_fetch_calib.json",
                 # L2 request bandwidth of the same launch (TCC_REQ x 128 B, PMC) against the L2 peak
                 "l2_achieved": round(l2_achieved, 1) if l2_achieved else None,
                 "l2_peak": L2_PEAK_GBS,
@@ -694,6 +737,8 @@ def main():
                                for m, c in (("closest", cl), ("shadow", sh))})}
     if dom == "path" and prof:
         roofline["latency"] = latency_model(prof, cl, sh, npix, value * 1e6)
+    if dom == "path":
+        roofline["time_split"] = time_split(pprof, counts)
     if achieved > HBM_PEAK_GBS:   # the model bytes are not HBM bytes: caches serve most of them
         roofline["note"] = ("the SURVEY.md §8d algorithmic bytes exceed the HBM peak: most node and triangle reads "
                             "hit L2 or the Infinity Cache (on C3 ~66 % L2 hits by PMC, profiles/r20g_summary.md; a small scene's BVH is wholly "

@@ -1,9 +1,14 @@
 """Summarise a tools/profile_driver.sh (or tools/profile.sh) run (rocprofv3 csv) into
 profiles/<tag>_summary.md, profiles/<tag>_traffic.json and copies of the kernel stats / counter csvs.
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and reads half the bytes of
-128-byte-line traffic on gfx950, so read traffic = 2 * FETCH_SIZE * 1024; WRITE_SIZE (KiB) is added
-unscaled; TCC_MISS * 128 B is printed beside it as the calibration check for this access pattern.
+HBM bytes: the L2 -> fabric read requests by size (pass `rq`: 32 x RDREQ_32B + 64 x RDREQ_64B +
+128 x RDREQ_128B) when the profile has them, else 2 * FETCH_SIZE * 1024.  tools/fetch_calib (profiles/
+r21_fetch_calib.json) calibrated both on the traversal's own widths: on gfx950 every fabric read request
+is 128 B whatever the access width (64-B nodes, 32-B leaf headers, 48-B triangles, the 128-B leaf
+batch), FETCH_SIZE tallies each at 64 B (its 128-B term, TCC_BUBBLE, reads 0), and one isolated record
+costs exactly one request per line it covers; so 2 x FETCH_SIZE = 128 x RDREQ for every width.  Reads
+to the Infinity Cache are counted too (RDREQ_DRAM = RDREQ): the figure bounds HBM traffic from above.
+WRITE_SIZE (KiB) is added unscaled; TCC_MISS * 128 B is printed beside it.
 
 The persistent path kernel renders every spp of its call in one launch, and bench.py launches it
 for the warmup, the timed render and an untimed breakdown.  Its record in traffic.json is the
@@ -19,7 +24,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-PASSES = ("fetch", "write", "tcc", "sq", "lat", "ea", "pmc_fetch", "pmc_write", "pmc_tcc")
+PASSES = ("fetch", "write", "tcc", "sq", "lat", "ea", "rq", "rq2", "pmc_fetch", "pmc_write", "pmc_tcc")
 
 
 def short(name):
@@ -79,7 +84,8 @@ def main(tag):
         if f.exists():
             passes[sub], m = read_pass(f)
             meta.update(m)
-    line = bench_line(src / "fetch.log") or bench_line(src / "pmc_fetch.log") or kt_line
+    line = (bench_line(src / "fetch.log") or bench_line(src / "pmc_fetch.log") or bench_line(src / "rq.log")
+            or kt_line)
     workload = line["config"] if line else None
     timed_spp = line["steps"] * line["config"].get("spp_per_step", 1) if line else None
 
@@ -105,13 +111,22 @@ def main(tag):
         if k in meta:
             rec["grid_threads"] = int(meta[k][5])
         c = rec["counters"]
-        if "FETCH_SIZE" in c:
+        if "TCC_EA0_RDREQ_128B_sum" in c:   # requests by size (calibrated, see the docstring)
+            rec["read_bytes"] = (32 * c.get("TCC_EA0_RDREQ_32B_sum", 0.0) + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+                                 + 128 * c["TCC_EA0_RDREQ_128B_sum"])
+            rec["read_bytes_source"] = "32/64/128 x TCC_EA0_RDREQ_{32B,64B,128B} (profiles/r21_fetch_calib.json)"
+            if "FETCH_SIZE" in c:
+                rec["read_over_fetch_size"] = rec["read_bytes"] / (c["FETCH_SIZE"] * 1024)
+        elif "FETCH_SIZE" in c:
             rec["read_bytes"] = 2 * c["FETCH_SIZE"] * 1024
+            rec["read_bytes_source"] = "2 x FETCH_SIZE (calibrated: profiles/r21_fetch_calib.json)"
+        if "read_bytes" in rec:
             rec["write_bytes"] = c.get("WRITE_SIZE", 0.0) * 1024
             rec["hbm_bytes_per_launch"] = rec["read_bytes"] + rec["write_bytes"]
             if is_path_kernel(k) and timed_spp:
                 rec["timed_spp"] = timed_spp
                 rec["hbm_bytes_per_spp"] = rec["hbm_bytes_per_launch"] / timed_spp
+                rec["read_bytes_per_spp"] = rec["read_bytes"] / timed_spp
         if "TCC_REQ_sum" in c:
             rec["l2_req_bytes_per_launch"] = c["TCC_REQ_sum"] * 128
             if is_path_kernel(k) and timed_spp:
@@ -149,7 +164,14 @@ def main(tag):
         if "TCP_TCC_READ_REQ_sum" in c and c["TCP_TCC_READ_REQ_sum"]:
             out.append(f"- TCP -> TCC read latency: {c['TCP_TCC_READ_REQ_LATENCY_sum'] / c['TCP_TCC_READ_REQ_sum']:.0f} cycles "
                        f"mean over {c['TCP_TCC_READ_REQ_sum']:.3g} requests")
-        if "TCC_EA0_RDREQ_sum" in c and c["TCC_EA0_RDREQ_sum"]:
+        if "TCC_EA0_RDREQ_128B_sum" in c:
+            out.append(f"- L2 -> fabric read requests by size: 32 B {c.get('TCC_EA0_RDREQ_32B_sum', 0):.4g}, 64 B "
+                       f"{c.get('TCC_EA0_RDREQ_64B_sum', 0):.4g}, 128 B {c['TCC_EA0_RDREQ_128B_sum']:.4g} "
+                       f"(read bytes {rec['read_bytes'] / 1e12:.3f} TB per launch)")
+        if "TCC_EA0_RDREQ_DRAM_sum" in c:
+            out.append(f"- requests destined for DRAM (Infinity Cache hits included): {c['TCC_EA0_RDREQ_DRAM_sum']:.4g}; "
+                       f"TCC_BUBBLE (FETCH_SIZE's 128-B term): {c.get('TCC_BUBBLE_sum', 0):.4g}")
+        if "TCC_EA0_RDREQ_LEVEL_sum" in c and c.get("TCC_EA0_RDREQ_sum"):
             out.append(f"- L2 -> fabric read requests: {c['TCC_EA0_RDREQ_sum']:.3g}, mean in flight x time / count = "
                        f"{c['TCC_EA0_RDREQ_LEVEL_sum'] / c['TCC_EA0_RDREQ_sum']:.0f} cycles per request")
     (dst / f"{tag}_traffic.json").write_text(json.dumps(
