@@ -476,10 +476,11 @@ class HipContext:
 
     def render_form_inputs(self) -> dict:
         """The last persistent render's form-choice inputs: pixels per resident lane,
-        and the pilot's rays and misses (-1: the choice did not read the pilot)."""
+        and the cost-ordering pilot's rays and mean traversal steps per ray (rays -1: not read)."""
         a, b, c = C.c_int64(0), C.c_int64(0), C.c_int64(0)
         self._check(self.lib.akr_hip_render_form_inputs(self.h, C.byref(a), C.byref(b), C.byref(c)))
-        return {"pixels_per_lane": a.value / 1000, "pilot_rays": b.value, "pilot_misses": c.value}
+        return {"pixels_per_lane": a.value / 1000, "pilot_rays": b.value,
+                "pilot_mean_steps": c.value / b.value if b.value > 0 else None}
 
     def path_profile(self) -> dict:
         """k_path phase profile of the counted launches since reset_stats (ticks: 100 MHz)."""

@@ -274,11 +274,11 @@ struct akr_hip_ctx {
     // (default 6.0).  1080p C3 on one MI355X: the whole frame has 7.9 pixels per lane (k_path 4.61 ms
     // against 4.85 for k_path_spec), a 2-way share 4.0 (2.55 against 2.48)
     int64_t path_tail_ppl10 = 60;
-    // option "path_tail_miss_pct": ... and at least this share (percent) of pilot camera rays missing
-    // the scene (C3 shares: ~45 %; the Cornell box at 1080p: 2.5-4.7 % per 8-way share, the frame's
-    // edges beside the box, where k_path runs an 8-way share in 0.276 ms against 0.300 for
-    // k_path_defer, profiles/r16_cornell_forms.log)
-    int path_tail_miss_pct = 15;
+    // option "path_tail_steps": ... and a cost-ordering pilot whose camera rays take at least this many
+    // traversal steps (wide-node visits + triangle tests) on average: long dependent-fetch chains, where
+    // a lane freed early can run work that overlaps them (DESIGN.md §3.12 gives the measured means of
+    // the soup's and the Cornell box's shares; the box's rays are a few steps long, its shares run k_path)
+    int path_tail_steps = 12;
     // explicit overrides of the rule's size test (0, default: pixels per lane): a tail form for renders
     // of at most this many pixels (options "path_spec_pixels", "path_defer_pixels"); option
     // "path_defer_min_tris" (0, default: no test) keeps scenes below it on k_path
@@ -294,10 +294,11 @@ struct akr_hip_ctx {
                                // speculation tree's levels; the r19 main line measured 2, 4, 8, 15 alike, 1 slower,
                                // profiles/r19_spec_depth.log)
     bool path_spec_alt = false;  // option "path_spec_alt": the tree's one-bounce branches too (measured slower)
-    // the last render's form inputs (akr_hip_render_form_inputs): pixels per lane x 1000, pilot rays, misses
-    int64_t last_ppl1000 = 0, last_pilot_rays = -1, last_pilot_miss = -1;
-    DBuf<uint32_t> d_miss;        // the pilot's miss count
-    uint32_t *h_miss = nullptr, *d_miss_host = nullptr;  // mapped host word it is copied into
+    // the last render's form inputs (akr_hip_render_form_inputs): pixels per lane x 1000, the pilot's
+    // rays and their summed steps
+    int64_t last_ppl1000 = 0, last_pilot_rays = -1, last_pilot_steps = -1;
+    DBuf<unsigned long long> d_steps_sum;   // the pilot's summed steps
+    uint32_t *h_sum = nullptr, *d_sum_host = nullptr;  // mapped host words it is copied into
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
     // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
@@ -413,7 +414,7 @@ struct akr_hip_ctx {
             if (e) (void)hipEventDestroy(e);
         if (h_remain) (void)hipHostFree(h_remain);
         if (h_check) (void)hipHostFree(h_check);
-        if (h_miss) (void)hipHostFree(h_miss);
+        if (h_sum) (void)hipHostFree(h_sum);
         if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_gather) (void)hipEventDestroy(ev_gather);
@@ -704,8 +705,9 @@ struct akr_hip_ctx {
         }
         d_owork.reserve(kTraceWords);
         d_ocnt.reserve(3);
+        d_steps_sum.reserve(1);
         d_otmp.reserve(pixel_order_tmp_bytes((uint32_t)std::min<size_t>(n, UINT32_MAX)));
-        if (path_order_pilot_spp > 0) d_pprobe.reserve(n);  // the path pilot's probe (option), ADVICE r4
+        d_pprobe.reserve(n);  // the tail pilot's and the path pilot's probe (no allocation in a render)
         cap = n;
     }
 
@@ -775,7 +777,7 @@ struct akr_hip_ctx {
     // decreasing pilot cost (tile order within a cost class).  The pilot traces the camera ray of
     // every slot's first sample with the counting kernel into scratch counters; nothing it does
     // reaches the film, the sampler states or the context's statistics.
-    void pixel_order(uint32_t N, hipStream_t ms, bool count_miss = false) {
+    void pixel_order(uint32_t N, hipStream_t ms, bool sum_steps = false) {
         // sized for the capacity by ensure_capacity (the sort's scratch grows with n), so no size
         // query runs per render
         if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
@@ -792,42 +794,19 @@ struct akr_hip_ctx {
         t.step_cap = (uint32_t)path_order_cap;
         // the steps-only build: no hits, no tallies (the counting build spilled and ran ~20 % longer)
         launch_trace(TRACE_PILOT, false, true, true, t, grid_for(TRACE_CLOSEST, n_rays), ms);
-        if (count_miss) {
-            d_miss.reserve(1);
-            HIPCHK(hipMemsetAsync(d_miss.p, 0, sizeof(uint32_t), ms));
-        }
+        if (sum_steps) HIPCHK(hipMemsetAsync(d_steps_sum.p, 0, sizeof(unsigned long long), ms));
         launch_order_keys(d_okey[1].p, N, (uint32_t)path_order_shift, (uint32_t)(path_order_classes - 1), sub,
-                          d_okey[0].p, d_oidx[0].p, ms, count_miss ? d_miss.p : nullptr);
+                          d_okey[0].p, d_oidx[0].p, ms, sum_steps ? d_steps_sum.p : nullptr);
         sort_pixel_order(d_otmp.p, tb, d_okey[0].p, d_okey[1].p, d_oidx[0].p, d_oidx[1].p, N, ms);
         HIPCHK(hipGetLastError());
     }
 
-    // The miss count of the pilot just issued on `ms` (pixel_order with count_miss), on the host: one
-    // word copied into mapped host memory, the host waiting for the stream (the render's form depends
-    // on it).
-    uint32_t read_pilot_miss(hipStream_t ms) {
-        if (!h_miss) {
-            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_miss), sizeof(uint32_t),
-                                 hipHostMallocMapped | hipHostMallocCoherent));
-            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_miss_host), h_miss, 0));
-        }
-        *reinterpret_cast<volatile uint32_t *>(h_miss) = kMappedSentinel;
-        launch_store_word(d_miss.p, d_miss_host, ms);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(ms));
-        const uint32_t m = read_mapped(h_miss);
-        if (m == kMappedSentinel) throw std::runtime_error("pilot: the device never reported its miss count");
-        return m;
-    }
-
-    // Path pilot: a counting k_path render of S samples per slot (the render's own first samples: a
-    // slot's sampler starts from its seed in every render) into the zeroed film, whose probe gives
-    // each slot's rays; the film is zeroed again for the render.  Classes of 2^shift rays.
-    void pixel_order_path(const PathArgs &base, bool tab, uint32_t grid, uint32_t N, int S, hipStream_t ms) {
-        // S samples trace at most S * (2 max_depth + 1) rays (max(1, max_depth) closest-hit, max_depth shadow)
-        const uint32_t max_rays = (uint32_t)S * (2u * (uint32_t)std::max(base.max_depth, 0) + 1u);
-        if (d_okey[0].n < N || d_oidx[0].n < N || d_pprobe.n < N)
-            throw std::runtime_error("pixel order buffers not sized");
+    // A counting k_path render of S samples per slot (the render's own first samples: a slot's sampler
+    // starts from its seed in every render) into the zeroed film, whose pixel probe d_pprobe then holds
+    // each slot's closest-hit and shadow rays; the film is zeroed again for the render.  Nothing of it
+    // reaches the context's statistics (scratch counters, no phase profile).
+    void probe_render(const PathArgs &base, bool tab, uint32_t N, int S, hipStream_t ms) {
+        if (d_pprobe.n < N) throw std::runtime_error("pilot probe buffer not sized");
         HIPCHK(hipMemsetAsync(d_owork.p, 0, kTraceWords * sizeof(uint32_t), ms));
         PathArgs pp = base;
         pp.spp = (uint32_t)S;
@@ -838,9 +817,41 @@ struct akr_hip_ctx {
         pp.probe_clock = 0;
         pp.order = nullptr;
         pp.fault_test = 0;
-        launch_path(true, PATH_PLAIN, tab, pp, std::min<uint32_t>(grid, path_grid[PATH_PLAIN][tab]), ms);
-        launch_probe_cost(d_pprobe.p, N, d_okey[1].p, ms);
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>(path_grid[PATH_PLAIN][tab], ((uint64_t)N + kTraceBlock - 1) / kTraceBlock));
+        launch_path(true, PATH_PLAIN, tab, pp, grid, ms);
         HIPCHK(hipMemsetAsync(d_film.p, 0, (size_t)N * sizeof(float4), ms));
+    }
+
+    // The pilot's summed steps (pixel_order with sum_steps) on the host: the two words copied into
+    // mapped host memory, the host waiting for the render's stream once
+    uint64_t read_steps_sum(hipStream_t ms) {
+        if (!h_sum) {
+            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_sum), 2 * sizeof(uint32_t),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_sum_host), h_sum, 0));
+        }
+        volatile uint32_t *hv = reinterpret_cast<volatile uint32_t *>(h_sum);
+        hv[0] = hv[1] = kMappedSentinel;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(d_steps_sum.p);
+        launch_store_word(w, d_sum_host, ms);
+        launch_store_word(w + 1, d_sum_host + 1, ms);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(ms));
+        const uint32_t lo = read_mapped(h_sum), hi = read_mapped(h_sum + 1);
+        if (lo == kMappedSentinel && hi == kMappedSentinel)
+            throw std::runtime_error("pilot: the device never reported its step sum");
+        return (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+
+    // Path pilot (option path_order_pilot_spp): slots ranked by the rays their first S samples take
+    // (probe_render), in classes of 2^shift rays.
+    void pixel_order_path(const PathArgs &base, bool tab, uint32_t N, int S, hipStream_t ms) {
+        if (d_okey[0].n < N || d_oidx[0].n < N) throw std::runtime_error("pixel order buffers not sized");
+        // S samples trace at most S * (2 max_depth + 1) rays (max(1, max_depth) closest-hit, max_depth shadow)
+        const uint32_t max_rays = (uint32_t)S * (2u * (uint32_t)std::max(base.max_depth, 0) + 1u);
+        probe_render(base, tab, N, S, ms);
+        launch_probe_cost(d_pprobe.p, N, d_okey[1].p, ms);
         uint32_t shift = 0;
         while (((max_rays + 1u) >> shift) > (uint32_t)path_order_classes) shift++;
         launch_order_keys(d_okey[1].p, N, shift, (uint32_t)(path_order_classes - 1), 0, d_okey[0].p, d_oidx[0].p, ms);
@@ -1093,7 +1104,7 @@ struct akr_hip_ctx {
                                                                  (uint64_t)path_grid_pct / 100) * kTraceBlock;
                 const int64_t ppl1000 = (int64_t)((N * 1000 + lanes / 2) / lanes);
                 last_ppl1000 = ppl1000;
-                last_pilot_rays = last_pilot_miss = -1;
+                last_pilot_rays = last_pilot_steps = -1;
                 // the first persistent render of a context runs the pilot once on a few pixels: its
                 // kernels (and rocPRIM's) are loaded then, not inside a later ordered render
                 if (path_order != 0 && !order_warm) {
@@ -1109,27 +1120,26 @@ struct akr_hip_ctx {
                 const bool pilot = path_order != 0 && p.spp >= order_min_spp && N >= 2 &&
                                    (path_order == 2 || (!forced || (path_spec != 1 && path_defer == 0)));
                 const bool path_pilot = pilot && path_order_pilot_spp > 0;
-                // the rule's size and scene tests; its miss test needs the camera-ray pilot
+                // the rule: its size and scene tests, then the camera-ray pilot's mean steps
                 const bool size_ok = ppl1000 <= path_tail_ppl10 * 100;
                 const bool tris_ok = path_defer_min_tris == 0 || (int64_t)n_tris() >= path_defer_min_tris;
-                const bool want_miss = !forced && path_order == 2 && pilot && !path_pilot && tris_ok &&
-                                       (path_spec == 2 ? (path_spec_pixels > 0 ? (int64_t)N <= path_spec_pixels : size_ok)
-                                                       : (path_defer_pixels > 0 ? (int64_t)N <= path_defer_pixels : size_ok));
+                const bool want_steps = !forced && path_order == 2 && pilot && !path_pilot && tris_ok &&
+                                        (path_spec == 2 ? (path_spec_pixels > 0 ? (int64_t)N <= path_spec_pixels : size_ok)
+                                                        : (path_defer_pixels > 0 ? (int64_t)N <= path_defer_pixels : size_ok));
                 if (pilot) {
                     if (path_pilot)
-                        timed("pilot", ms, [&] { pixel_order_path(pa, tab, std::max<uint32_t>(1, path_grid[PATH_PLAIN][tab]),
-                                                                  (uint32_t)N, path_order_pilot_spp, ms); });
+                        timed("pilot", ms, [&] { pixel_order_path(pa, tab, (uint32_t)N, path_order_pilot_spp, ms); });
                     else
-                        timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms, want_miss); });
+                        timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms, want_steps); });
                     pa.order = d_oidx[1].p;
                 }
                 bool tail = false;
-                if (want_miss) {  // the host waits for the pilot's miss count (a few hundred microseconds)
+                if (want_steps) {  // the host waits for the pilot (well under a millisecond at a rank share)
                     const uint64_t rays = ((uint64_t)N + (1u << path_order_sub) - 1) >> path_order_sub;
-                    const uint32_t miss = read_pilot_miss(ms);
+                    const uint64_t steps = read_steps_sum(ms);
                     last_pilot_rays = (int64_t)rays;
-                    last_pilot_miss = miss;
-                    tail = (uint64_t)miss * 100 >= (uint64_t)path_tail_miss_pct * rays && miss > 0;
+                    last_pilot_steps = (int64_t)steps;
+                    tail = steps >= (uint64_t)path_tail_steps * rays;
                 }
                 int kind = PATH_PLAIN;
                 if (path_spec == 1) kind = PATH_SPEC;
@@ -1515,7 +1525,6 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_order_pilot_spp") {
             if (value < 0 || value > 64) throw std::runtime_error("path_order_pilot_spp must be in [0, 64]");
             ctx->path_order_pilot_spp = (int)value;
-            if (value > 0) ctx->cap = 0;  // the next render's ensure_capacity reserves the pilot's probe
         } else if (k == "path_spec_alt") {
             ctx->path_spec_alt = value != 0;
         } else if (k == "path_spec_depth") {
@@ -1530,9 +1539,9 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_tail_ppl10") {
             if (value < 0) throw std::runtime_error("path_tail_ppl10 must be >= 0");
             ctx->path_tail_ppl10 = value;
-        } else if (k == "path_tail_miss_pct") {
-            if (value < 0 || value > 100) throw std::runtime_error("path_tail_miss_pct must be in [0, 100]");
-            ctx->path_tail_miss_pct = (int)value;
+        } else if (k == "path_tail_steps") {
+            if (value < 0 || value > 4096) throw std::runtime_error("path_tail_steps must be in [0, 4096]");
+            ctx->path_tail_steps = (int)value;
         } else if (k == "path_spec_pixels") {
             if (value < 0) throw std::runtime_error("path_spec_pixels must be >= 0");
             ctx->path_spec_pixels = value;
@@ -2219,11 +2228,11 @@ int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered) {
 }
 
 int akr_hip_render_form_inputs(akr_hip_ctx *ctx, int64_t *pixels_per_lane_x1000, int64_t *pilot_rays,
-                               int64_t *pilot_misses) {
+                               int64_t *pilot_steps) {
     return guard(ctx, [&] {
         if (pixels_per_lane_x1000) *pixels_per_lane_x1000 = ctx->last_ppl1000;
         if (pilot_rays) *pilot_rays = ctx->last_pilot_rays;
-        if (pilot_misses) *pilot_misses = ctx->last_pilot_miss;
+        if (pilot_steps) *pilot_steps = ctx->last_pilot_steps;
     });
 }
 

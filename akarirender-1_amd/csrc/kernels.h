@@ -37,13 +37,10 @@ void launch_probe_cost(const uint4 *probe, uint32_t n, uint32_t *cost, hipStream
 // the key is one byte, so the radix sort is a single 8-bit pass (12-bit classes took 17 kernel launches,
 // ~0.11 ms; the pilot's 64-step cap at the default shift 2 needs 17 classes)
 constexpr uint32_t kOrderClassBits = 5, kOrderClassMask = (1u << kOrderClassBits) - 1u;
-// The steps-only pilot marks a ray that missed the scene (ended without a hit before its step cap)
-// with this bit of its step count; k_order_keys masks it and, given `miss`, counts the marked rays.
-constexpr uint32_t kPilotMissBit = 0x40000000u;
 void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, uint32_t sub, float4 *rays,
                        hipStream_t st);
 void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t cmax, uint32_t sub, uint32_t *key,
-                       uint32_t *idx, hipStream_t st, uint32_t *miss = nullptr);
+                       uint32_t *idx, hipStream_t st, unsigned long long *sum = nullptr);
 size_t pixel_order_tmp_bytes(uint32_t n);
 void sort_pixel_order(void *tmp, size_t tmp_bytes, const uint32_t *key_in, uint32_t *key_out, const uint32_t *idx_in,
                       uint32_t *idx_out, uint32_t n, hipStream_t st);

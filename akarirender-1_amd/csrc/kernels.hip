@@ -705,12 +705,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             if (busy && ((ANY && occluded) || cur == AKR_CHILD_EMPTY)) {
                 busy = false;
                 if constexpr (MODE != TRACE_PILOT) emit_result<MODE>(a, idx, best, bu, bv, bgid, occluded);
-                if (STEPS && a.ray_steps) {
-                    // the pilot flags a camera ray that left the scene (not one its step cap stopped):
-                    // the render's form choice counts them (capi.hip)
-                    const bool miss = MODE == TRACE_PILOT && bgid == kNoHit && !(a.step_cap && steps >= a.step_cap);
-                    a.ray_steps[idx] = steps | (miss ? kPilotMissBit : 0u);
-                }
+                if (STEPS && a.ray_steps) a.ray_steps[idx] = steps;
                 if (COUNT) c_deep += deep ? 1 : 0;
             }
         }
@@ -2884,24 +2879,26 @@ __global__ __launch_bounds__(kBlock) void k_pilot_rays(CameraDev cam, const uint
 // Sort key of slot i: its XCD shard above its cost class (steps >> shift, capped at cmax <=
 // kOrderClassMask, descending), so a stable sort orders each shard by decreasing cost and keeps tile
 // order within a class (few classes keep more of the tile order: a smaller cache footprint).
-// With `miss` set, the pilot rays flagged as misses (kPilotMissBit) are counted: one atomic per wave.
+// With `sum` set, the pilot rays' steps are summed (one atomic per wave; a ray the exact walk traced
+// adds nothing): the form rule's mean steps per camera ray (capi.hip).
 __global__ __launch_bounds__(kBlock) void k_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t cmax,
-                                                       uint32_t sub, uint32_t *key, uint32_t *idx, uint32_t *miss) {
+                                                       uint32_t sub, uint32_t *key, uint32_t *idx,
+                                                       unsigned long long *sum) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    bool m = false;
+    uint32_t add = 0;
     if (i < n) {
         uint32_t sh = 0;
         for (uint32_t k = 1; k < kWorkShards; k++) sh += i >= shard_begin(n, k) ? 1u : 0u;
         const uint32_t s = steps[i >> sub];  // 0xFFFFFFFF: traced by the exact BVH2 walk (rare): costliest class
-        const uint32_t cls = s == 0xFFFFFFFFu ? cmax : min((s & ~kPilotMissBit) >> shift, cmax);
+        const uint32_t cls = s == 0xFFFFFFFFu ? cmax : min(s >> shift, cmax);
         key[i] = (sh << kOrderClassBits) | (kOrderClassMask - cls);
         idx[i] = i;
-        // one pilot ray per 2^sub slots: count it at its first slot
-        m = s != 0xFFFFFFFFu && (s & kPilotMissBit) && (i & ((1u << sub) - 1u)) == 0u;
+        // one pilot ray per 2^sub slots: counted at its first slot
+        add = (s != 0xFFFFFFFFu && (i & ((1u << sub) - 1u)) == 0u) ? s : 0u;
     }
-    if (miss) {
-        const uint64_t b = __ballot(m);
-        if (b && __lane_id() == (uint32_t)(__ffsll((unsigned long long)b) - 1)) atomicAdd(miss, (uint32_t)__popcll(b));
+    if (sum) {
+        const unsigned long long w = wave_sum(add);
+        if (__lane_id() == 0 && w) atomicAdd(sum, w);
     }
 }
 
@@ -3061,10 +3058,10 @@ void launch_pilot_rays(const CameraDev &cam, const uint32_t *pixel, uint32_t n, 
     hipLaunchKernelGGL(k_pilot_rays, dim3(blocks_for(n)), dim3(kBlock), 0, st, cam, pixel, n, sub, rays);
 }
 void launch_order_keys(const uint32_t *steps, uint32_t n, uint32_t shift, uint32_t cmax, uint32_t sub, uint32_t *key,
-                       uint32_t *idx, hipStream_t st, uint32_t *miss) {
+                       uint32_t *idx, hipStream_t st, unsigned long long *sum) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_order_keys, dim3(blocks_for(n)), dim3(kBlock), 0, st, steps, n, shift,
-                       cmax < kOrderClassMask ? cmax : kOrderClassMask, sub, key, idx, miss);
+                       cmax < kOrderClassMask ? cmax : kOrderClassMask, sub, key, idx, sum);
 }
 void launch_probe_cost(const uint4 *probe, uint32_t n, uint32_t *cost, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_probe_cost, dim3(blocks_for(n)), dim3(kBlock), 0, st, probe, n, cost);

@@ -215,7 +215,7 @@ const char *akr_hip_last_error(const akr_hip_ctx *ctx);
  * Render forms and their tuning (all give the same bits): "path" (0 wavefront,
  * 1 persistent kernel, 2 auto), "path_auto_pixels", "path_auto_complex";
  * the persistent form: "path_spec" (k_path_spec: 1 always, 0 never, 2 auto), "path_defer" (k_path_defer:
- * 1 forced, 0 k_path forced, 2 auto), the auto rule's "path_tail_ppl10" and "path_tail_miss_pct" and its
+ * 1 forced, 0 k_path forced, 2 auto), the auto rule's "path_tail_ppl10" and "path_tail_steps" and its
  * overrides "path_spec_pixels", "path_defer_pixels", "path_defer_min_tris"; k_path_spec's "path_spec_depth",
  * "path_spec_alt", "path_spec_fetch", "path_spec_fetch_pixels";
  * "path_tab", "path_mix", "path_min_wait", "path_grid_pct", "path_prio";
@@ -335,10 +335,10 @@ int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
 #define AKR_FORM_PATH_SPEC 4
 int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered);
 /* The inputs of the last persistent render's form choice: its pixels per resident
- * lane x 1000, and the pilot's camera rays and how many of them missed the scene (-1 when the choice
- * did not read the pilot: a forced form, no pilot, or a render too large for a tail form). */
+ * lane x 1000, and the cost-ordering pilot's camera rays and their summed traversal steps; -1 when the
+ * choice did not read the pilot (a forced form, no cost order, or a render too large for a tail form). */
 int akr_hip_render_form_inputs(akr_hip_ctx *ctx, int64_t *pixels_per_lane_x1000, int64_t *pilot_rays,
-                               int64_t *pilot_misses);
+                               int64_t *pilot_steps);
 int akr_hip_synchronize(akr_hip_ctx *ctx);
 /* Copies the first n records of the last render's pixel probe (see akr_pixel_probe); fails when
  * the last render ran without option "pixel_probe" or has fewer slots. */

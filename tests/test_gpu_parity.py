@@ -604,7 +604,7 @@ def test_spec_and_order_options_are_validated(hip_ctx_factory):
     with hip_ctx_factory(0) as ctx:
         for key, good, bad in (("path_spec_depth", (1, 3), (0, 4)), ("path_spec_fetch", (-1, 3), (-2, 5)),
                                ("path_order_pilot_spp", (0, 64), (-1, 65)), ("path_spec_fetch_pixels", (0, 1 << 40), (-1,)),
-                               ("path_tail_ppl10", (0, 1 << 40), (-1,)), ("path_tail_miss_pct", (0, 100), (-1, 101)),
+                               ("path_tail_ppl10", (0, 1 << 40), (-1,)), ("path_tail_steps", (0, 4096), (-1, 4097)),
                                ("wave_order", (0, 1), ()), ("path_spec_alt", (0, 1), ())):
             for v in good:
                 ctx.set_option(key, v)
@@ -633,31 +633,32 @@ def test_auto_form_by_shading(hip_ctx_factory):
                 # 3 spp: no pilot, so the constant-shading scene takes k_path
                 assert ctx.render_form()["form"] == ("k_path" if (simple or complex_ok) else "wavefront")
     # the persistent form by the pilot rule: a tail form (k_path_spec, or
-    # k_path_defer with path_spec 0) for a render of few pixels per resident lane whose pilot camera
-    # rays miss the scene often enough; k_path otherwise, and without a pilot
+    # k_path_defer with path_spec 0) for a render of few pixels per resident lane whose cost-ordering
+    # pilot finds long camera rays; k_path otherwise, and without a pilot
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
         tiles = [(0, 0, 48, 27)]
         _check_render(ctx, orc, 3, 5, tiles, 48, 27)     # below the order's 16-spp floor: no pilot
         assert ctx.render_form() == {"form": "k_path", "ordered": False}
-        assert ctx.render_form_inputs()["pilot_misses"] == -1
+        assert ctx.render_form_inputs()["pilot_rays"] == -1
+        ctx.set_option("path_tail_steps", 1)   # a bar every camera ray of the soup clears
         _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         inp = ctx.render_form_inputs()
-        assert inp["pilot_rays"] == 48 * 27 and 0.15 * 48 * 27 <= inp["pilot_misses"] < 48 * 27, inp
+        assert inp["pilot_rays"] == 48 * 27 and inp["pilot_mean_steps"] >= 1, inp
         assert 0 < inp["pixels_per_lane"] < 0.01
         assert ctx.render_form() == {"form": "k_path_spec", "ordered": True}
         ctx.set_option("path_spec", 0)    # the rule's tail form is then the deferred one
         _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}
         ctx.set_option("path_spec", 2)
-        ctx.set_option("path_tail_miss_pct", 100)   # too few misses: k_path
+        ctx.set_option("path_tail_steps", 4096)   # camera rays too short: k_path
         _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         assert ctx.render_form() == {"form": "k_path", "ordered": True}
-        ctx.set_option("path_tail_miss_pct", 15)
+        ctx.set_option("path_tail_steps", 1)
         ctx.set_option("path_tail_ppl10", 0)        # too many pixels per lane: k_path, the pilot not read
         _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         assert ctx.render_form() == {"form": "k_path", "ordered": True}
-        assert ctx.render_form_inputs()["pilot_misses"] == -1
+        assert ctx.render_form_inputs()["pilot_rays"] == -1
         ctx.set_option("path_tail_ppl10", 60)
         ctx.set_option("path_spec_pixels", 1000)    # the explicit size override (1296 pixels > 1000)
         _check_render(ctx, orc, 16, 5, tiles, 48, 27)

@@ -54,7 +54,7 @@ def main():
             best = min(ms_per_spp(tiles, args.spp) for _ in range(args.repeat))
             inp, form = ctx.render_form_inputs(), ctx.render_form()
             rows.append({"px": dist.n_pixels(tiles), "ms": round(best, 4), "form": form["form"],
-                         "miss": round(inp["pilot_misses"] / inp["pilot_rays"], 3) if inp["pilot_rays"] > 0 else None})
+                         "pilot_mean_steps": inp["pilot_mean_steps"]})
         ms = [r["ms"] for r in rows]
         print(json.dumps({"partition": name, "max_ms": max(ms), "sum_ms": round(sum(ms), 3),
                           "mean_ms": round(sum(ms) / len(ms), 4), "shares": rows}), flush=True)
