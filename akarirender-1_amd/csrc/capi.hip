@@ -279,6 +279,12 @@ struct akr_hip_ctx {
     // a lane freed early can run work that overlaps them (DESIGN.md §3.12 gives the measured means of
     // the soup's and the Cornell box's shares; the box's rays are a few steps long, its shares run k_path)
     int path_tail_steps = 12;
+    // option "path_cache_mb": a BVH of at most this many MiB on the device (wide nodes + leaf blob) is
+    // taken as cache-resident (half the 256-MiB Infinity Cache: the kernel streams its film and rays
+    // beside it, MI355X_MICROARCH.md §Infinity Cache): its rule form is k_path_defer at every size
+    // (soups of 100K triangles, ~15 MB: 4-20 % faster than k_path; 1M, ~150 MB, and 10M, ~1.5 GB, take
+    // k_path_spec on rank shares)
+    int64_t path_cache_mb = 128;
     // explicit overrides of the rule's size test (0, default: pixels per lane): a tail form for renders
     // of at most this many pixels (options "path_spec_pixels", "path_defer_pixels"); option
     // "path_defer_min_tris" (0, default: no test) keeps scenes below it on k_path
@@ -386,6 +392,11 @@ struct akr_hip_ctx {
     bool wide = true;         // 4-wide quantized traversal (false: BVH2 kernel only, for A/B)
     bool lean = true;         // fused per-node slot-test arithmetic (kernels.hip visit_wide_lean; false: A/B)
     int wide_collapse = AKR_COLLAPSE_SAH;  // akr_build_params::wide_collapse of the last build
+    // option "leaf_align" (taken by the next build or import): each leaf record of the device blob
+    // starts on a multiple of this many 16-B words (1 = packed; 8 = a 128-B line, so a leaf of at
+    // most two triangles is one fabric request and the leaf phase's eight-load batch never straddles
+    // two lines, tools/fetch_calib: a straddling 128-B gather costs 1.4 requests per line)
+    int leaf_align = 1;
     bool ray_steps = false;   // diagnostic: standalone traces record per-ray iterations (counted kernel)
     DBuf<uint32_t> d_steps;
     uint64_t n_steps = 0;
@@ -1123,9 +1134,13 @@ struct akr_hip_ctx {
                 // the rule: its size and scene tests, then the camera-ray pilot's mean steps
                 const bool size_ok = ppl1000 <= path_tail_ppl10 * 100;
                 const bool tris_ok = path_defer_min_tris == 0 || (int64_t)n_tris() >= path_defer_min_tris;
-                const bool want_steps = !forced && path_order == 2 && pilot && !path_pilot && tris_ok &&
-                                        (path_spec == 2 ? (path_spec_pixels > 0 ? (int64_t)N <= path_spec_pixels : size_ok)
-                                                        : (path_defer_pixels > 0 ? (int64_t)N <= path_defer_pixels : size_ok));
+                // the BVH's device bytes against the Infinity Cache share: a cache-resident
+                // tree takes k_path_defer at any size, a larger one k_path_spec up to path_tail_ppl10
+                const uint64_t bvh_bytes = (uint64_t)d_wnodes.n * sizeof(akr_bvh4_node) + (uint64_t)d_wleaves.n * sizeof(float4);
+                const bool cache_resident = path_spec != 1 && p.max_depth <= 8 && bvh_bytes <= (uint64_t)path_cache_mb << 20;
+                const bool size_tail = path_spec == 2 ? (path_spec_pixels > 0 ? (int64_t)N <= path_spec_pixels : size_ok)
+                                                      : (path_defer_pixels > 0 ? (int64_t)N <= path_defer_pixels : size_ok);
+                const bool want_steps = !forced && path_order == 2 && pilot && !path_pilot && tris_ok && (cache_resident || size_tail);
                 if (pilot) {
                     if (path_pilot)
                         timed("pilot", ms, [&] { pixel_order_path(pa, tab, (uint32_t)N, path_order_pilot_spp, ms); });
@@ -1144,7 +1159,9 @@ struct akr_hip_ctx {
                 int kind = PATH_PLAIN;
                 if (path_spec == 1) kind = PATH_SPEC;
                 else if (path_defer == 1 && p.max_depth <= 8) kind = PATH_DEFER;
-                else if (path_defer == 2 && tail) kind = path_spec == 2 ? PATH_SPEC : (p.max_depth <= 8 ? PATH_DEFER : PATH_PLAIN);
+                else if (path_defer == 2 && tail)
+                    kind = cache_resident ? PATH_DEFER
+                                    : (path_spec == 2 ? PATH_SPEC : (p.max_depth <= 8 ? PATH_DEFER : PATH_PLAIN));
                 const uint64_t resident = (uint64_t)path_grid[kind][tab] * (uint64_t)path_grid_pct / 100;
                 const uint32_t grid = (uint32_t)std::max<uint64_t>(
                     1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
@@ -1539,6 +1556,12 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_tail_ppl10") {
             if (value < 0) throw std::runtime_error("path_tail_ppl10 must be >= 0");
             ctx->path_tail_ppl10 = value;
+        } else if (k == "leaf_align") {
+            if (value != 1 && value != 2 && value != 4 && value != 8) throw std::runtime_error("leaf_align must be 1, 2, 4 or 8");
+            ctx->leaf_align = (int)value;
+        } else if (k == "path_cache_mb") {
+            if (value < 0) throw std::runtime_error("path_cache_mb must be >= 0");
+            ctx->path_cache_mb = value;
         } else if (k == "path_tail_steps") {
             if (value < 0 || value > 4096) throw std::runtime_error("path_tail_steps must be in [0, 4096]");
             ctx->path_tail_steps = (int)value;
@@ -1710,7 +1733,9 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         const auto &leaves = ctx->bvh4.leaves;
         std::vector<uint32_t> leaf_off(leaves.size());
         size_t words = 0;
+        const size_t align = (size_t)std::max(1, ctx->leaf_align);
         for (size_t i = 0; i < leaves.size(); i++) {
+            words = (words + align - 1) / align * align;
             if (words >= AKR_CHILD_LEAF) break;
             leaf_off[i] = (uint32_t)words;
             words += 2 + 3 * (size_t)leaves[i].count;
@@ -1720,7 +1745,8 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         // record with the header whatever the leaf's count (kernels.hip path_leaf)
         const size_t pad = 3;
         std::unique_ptr<float4[]> blob(new float4[words + pad]);
-        std::memset(static_cast<void *>(blob.get() + words), 0, sizeof(float4) * pad);
+        if (align > 1) std::memset(static_cast<void *>(blob.get()), 0, sizeof(float4) * (words + pad));  // the gaps
+        else std::memset(static_cast<void *>(blob.get() + words), 0, sizeof(float4) * pad);
         const float4 *tri4 = reinterpret_cast<const float4 *>(b.tris.data());
         std::vector<akr_bvh4_node> wn = ctx->bvh4.nodes;
         auto remap = [&](uint32_t r) {

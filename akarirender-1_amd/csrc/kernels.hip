@@ -1495,8 +1495,9 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
             // the counting build splits the iteration's time: issue, wait, work
             const bool vis = busy && is_internal(r.cur);
             const unsigned long long ta = wall_clock64();
-            WideNode nd{};
-            if (vis) nd = wide_load(wn, r.cur);
+            // every lane loads (an idle lane node 0, a cache hit): a load under a branch makes the
+            // compiler wait for it inside the branch, before the clock below
+            const WideNode nd = wide_load(wn, vis ? r.cur : 0u);
             const unsigned long long tb = wall_clock64();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             tc = wall_clock64();
@@ -1608,18 +1609,10 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
         bool hit_any = false;
         const unsigned long long ta = wall_clock64();
         const bool in_leaf = busy && r.leaf != AKR_CHILD_EMPTY;
-        const float4 *lr = wide_leaves + (r.leaf & 0x7FFFFFFFu);
-        float4 l0{}, l1{}, pa0{}, pb0{}, pc0{}, pa1{}, pb1{}, pc1{};
-        if (in_leaf) {
-            l0 = lr[0];
-            l1 = lr[1];
-            pa0 = lr[2];
-            pb0 = lr[3];
-            pc0 = lr[4];
-            pa1 = lr[5];
-            pb1 = lr[6];
-            pc1 = lr[7];
-        }
+        // every lane loads (a lane without a leaf the blob's first record: see path_traverse)
+        const float4 *lr = wide_leaves + (in_leaf ? (r.leaf & 0x7FFFFFFFu) : 0u);
+        const float4 l0 = lr[0], l1 = lr[1], pa0 = lr[2], pb0 = lr[3], pc0 = lr[4], pa1 = lr[5], pb1 = lr[6],
+                     pc1 = lr[7];
         const unsigned long long tb = wall_clock64();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long tc = wall_clock64();

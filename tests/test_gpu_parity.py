@@ -84,13 +84,15 @@ def test_trace_builder_independent(hip_ctx_factory):
         assert np.array_equal(gh["t"][both], bh["t"][both])
 
 
-@pytest.mark.parametrize("leaf", [1, 2, 8])
-def test_trace_leaf_sizes(hip_ctx_factory, leaf):
+@pytest.mark.parametrize("leaf,align", [(1, 1), (2, 1), (8, 1), (1, 8), (4, 4), (8, 8)])
+def test_trace_leaf_sizes(hip_ctx_factory, leaf, align):
     """Leaves of 1, 2 and up to 8 triangles: the leaf phases fetch the second triangle record with the
-    header whatever the count (a one-triangle leaf reads into the next leaf or the blob's padding), and
-    read the third and later ones in the loop; closest-hit and any-hit traces, and renders through both
+    header whatever the count (a one-triangle leaf reads into the next leaf, the alignment gap or the
+    blob's padding), and read the third and later ones in the loop; leaf records packed or aligned to
+    64 / 128 B (option leaf_align); closest-hit and any-hit traces, and renders through the three
     persistent kernels (final sampler states too)."""
     with hip_ctx_factory(0) as ctx:
+        ctx.set_option("leaf_align", align)
         cs, orc = _setup(ctx, small_soup(30_000), max_leaf_size=leaf)
         assert ctx.accel_info().max_leaf <= leaf
         _check_trace(ctx, orc, cs, random_rays(1 << 14, 4, -1.1, 1.1), False)
@@ -604,7 +606,8 @@ def test_spec_and_order_options_are_validated(hip_ctx_factory):
     with hip_ctx_factory(0) as ctx:
         for key, good, bad in (("path_spec_depth", (1, 3), (0, 4)), ("path_spec_fetch", (-1, 3), (-2, 5)),
                                ("path_order_pilot_spp", (0, 64), (-1, 65)), ("path_spec_fetch_pixels", (0, 1 << 40), (-1,)),
-                               ("path_tail_ppl10", (0, 1 << 40), (-1,)), ("path_tail_steps", (0, 4096), (-1, 4097)),
+                               ("path_tail_ppl10", (0, 1 << 40), (-1,)), ("path_tail_steps", (0, 4096), (-1, 4097)), ("path_cache_mb", (0, 1 << 20), (-1,)),
+                               ("leaf_align", (1, 8), (0, 3, 16)),
                                ("wave_order", (0, 1), ()), ("path_spec_alt", (0, 1), ())):
             for v in good:
                 ctx.set_option(key, v)
@@ -632,9 +635,10 @@ def test_auto_form_by_shading(hip_ctx_factory):
                 assert set(ctx.kernel_stats()) == {want}, (sc, complex_ok, ctx.kernel_stats())
                 # 3 spp: no pilot, so the constant-shading scene takes k_path
                 assert ctx.render_form()["form"] == ("k_path" if (simple or complex_ok) else "wavefront")
-    # the persistent form by the pilot rule: a tail form (k_path_spec, or
-    # k_path_defer with path_spec 0) for a render of few pixels per resident lane whose cost-ordering
-    # pilot finds long camera rays; k_path otherwise, and without a pilot
+    # the persistent form by the pilot rule: for a scene whose camera rays take long
+    # traversals (the cost-ordering pilot's mean steps), k_path_defer when the BVH is cache-resident,
+    # else k_path_spec (k_path_defer with path_spec 0) for a render of few pixels per resident lane;
+    # k_path otherwise, and without a pilot
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
         tiles = [(0, 0, 48, 27)]
@@ -646,6 +650,9 @@ def test_auto_form_by_shading(hip_ctx_factory):
         inp = ctx.render_form_inputs()
         assert inp["pilot_rays"] == 48 * 27 and inp["pilot_mean_steps"] >= 1, inp
         assert 0 < inp["pixels_per_lane"] < 0.01
+        assert ctx.render_form() == {"form": "k_path_defer", "ordered": True}   # a 20K soup's BVH: cache-resident
+        ctx.set_option("path_cache_mb", 0)     # as if it were not
+        _check_render(ctx, orc, 16, 5, tiles, 48, 27)
         assert ctx.render_form() == {"form": "k_path_spec", "ordered": True}
         ctx.set_option("path_spec", 0)    # the rule's tail form is then the deferred one
         _check_render(ctx, orc, 16, 5, tiles, 48, 27)

@@ -15,6 +15,9 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "akarirender-1_amd"))
 
 
+BUILD_OPTS = {"leaf_align"}   # options read when the BVH is built or imported
+
+
 def parse(cfg: str):
     out = {}
     for kv in (x for x in cfg.split(",") if x):
@@ -42,12 +45,18 @@ def main():
     ctxs = []
     t0 = time.time()
     base = capi.HipContext(0)
+    for key, v in parse(args.configs[0]).items():   # build-time options take effect at the upload
+        if key in BUILD_OPTS:
+            base.set_option(key, v)
     scene.upload_scene(base, cs, builder=capi.BUILDER_SBVH, n_threads=16)
     nodes, tris = base.accel_export()
     print(f"built in {time.time() - t0:.1f} s", flush=True)
     for k, cfg in enumerate(args.configs):
         c = base if k == 0 else capi.HipContext(0)
         if k:
+            for key, v in parse(cfg).items():
+                if key in BUILD_OPTS:
+                    c.set_option(key, v)
             scene.upload_scene(c, cs, bvh=(nodes, tris), n_threads=16)
         for key, v in parse(cfg).items():
             c.set_option(key, v)
