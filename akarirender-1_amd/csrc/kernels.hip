@@ -144,6 +144,18 @@ typedef __attribute__((address_space(1))) unsigned long long glb_u64;
 // re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
 __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_u64 *ovf, uint32_t ovf_threads,
                                               uint32_t tid, uint32_t gtid, int &sp, float lim) {
+#ifdef AKR_POP2  // A/B build: the top two LDS entries in one ds_read2st64 (one round trip for a culled top)
+    while (sp >= 2 && sp <= kStackLds) {
+        const unsigned long long e1 = s_stack[(sp - 1) * kTraceBlock + tid];
+        const unsigned long long e2 = s_stack[(sp - 2) * kTraceBlock + tid];
+        if (!(__uint_as_float((uint32_t)(e1 >> 32)) > lim)) {
+            sp -= 1;
+            return (uint32_t)e1;
+        }
+        sp -= 2;
+        if (!(__uint_as_float((uint32_t)(e2 >> 32)) > lim)) return (uint32_t)e2;
+    }
+#endif
     while (sp > 0) {
         --sp;
         unsigned long long e;
@@ -1462,6 +1474,10 @@ __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
 #define AKR_PATH_WAVES 4
 #endif
 
+__device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
+    return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
 // One lane's ray in the persistent path kernels' traversal loop (k_trace's registers) and the
 // counting build's tallies ([0] closest-hit rays, [1] shadow rays).
 struct PathRay {
@@ -1921,6 +1937,18 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #ifdef AKR_PROBE_NOSHADOW  // timing probe only (not exact): shadow rays are not traced
                     bo.sh = false;
 #endif
+#ifdef AKR_NEXT_SELECT  // A/B build: value selects instead of branches (0 VGPRs spilled, the Bounce in scratch)
+                    const bool bsh = bo.sh, bext = bo.ext;
+                    ra = sel4(bsh, bo.s0, bo.e0);
+                    rb = sel4(bsh, bo.s1, bo.e1);
+                    scol = bsh ? bo.col : scol;
+                    pe0 = sel4(bsh, bo.e0, pe0);
+                    pe1 = sel4(bsh, bo.e1, pe1);
+                    pend = bsh ? bext : pend;
+                    next_any = bsh;
+                    fresh = bsh || bext;
+                    sample_end = !(bsh || bext);
+#else
                     if (bo.sh) {  // the shadow ray first, the extension ray waits behind it
                         ra = bo.s0;
                         rb = bo.s1;
@@ -1937,6 +1965,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     } else {
                         sample_end = true;
                     }
+#endif
                 }
             }
             if (COUNT) p_tsh += wall_clock64() - p_ts;
