@@ -1498,10 +1498,15 @@ struct PathCount {
 };
 
 // B. k_trace's traversal phase over every busy lane's ray (all rays here are lean)
-template <bool COUNT>
+// PRIO (k_path_spec, A/B build AKR_SPEC_PRIO): lanes running a speculative sample (`lowp`) do not
+// hold the wave in the loop while a committed-path lane is busy: the early exit counts only the
+// others' searching lanes.
+template <bool COUNT, bool PRIO = false>
 __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, const float4 *wn, lds_u64 *s_stack,
                                               glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
-                                              PathCount &c) {
+                                              PathCount &c, bool lowp = false) {
+    bool counted = true;  // this lane's search counts for the early exit
+    if constexpr (PRIO) counted = !lowp || __ballot(busy && !lowp) == 0;
     while (true) {
         [[maybe_unused]] unsigned long long tc = 0;
         if constexpr (COUNT) {
@@ -1534,7 +1539,7 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
             r.leaf = r.cur;  // postpone the leaf and keep descending
             r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
         }
-        const unsigned long long searching = __ballot(busy && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
+        const unsigned long long searching = __ballot(busy && counted && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
         if constexpr (COUNT) {
             const bool stop = (uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
                               (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0);
@@ -2800,7 +2805,12 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         idle_rounds = 0;
         // ---- B. traversal phase, C. leaf phase (k_trace's, shared with the other persistent kernels)
         const int kd = s.any() ? 1 : 0;
+#ifdef AKR_SPEC_PRIO
+        path_traverse<COUNT, true>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c,
+                                   s.node() != 0u);
+#else
         path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
+#endif
         if (COUNT) {
             const unsigned long long t = wall_clock64();
             p_tt += t - p_t;
