@@ -36,12 +36,20 @@ def main():
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--tile", type=int, default=64, help="tile size of the split (bench.py's default; 32 before r20)")
     ap.add_argument("--configs", nargs="+", default=[""])
+    ap.add_argument("--scene", choices=["soup", "cornell", "hall"], default="soup",
+                    help="cornell: the C2 box at 1080p; hall: the C4 stand-in at 4K (ADVICE r4: wave_order there)")
     args = ap.parse_args()
     import torch
     from akari_amd import capi, dist, scene
-    W, H = 1920, 1080
+    W, H = (3840, 2160) if args.scene == "hall" else (1920, 1080)
     dev = torch.device("cuda", 0)
-    cs = scene.compile_scene(scene.soup_scene(n_tris=args.tris, resolution=(W, H)))
+    if args.scene == "cornell":
+        sc = scene.cornell_scene(ROOT / "tests" / "golden" / "CornellBox-Original.obj.mesh", resolution=(W, H))
+    elif args.scene == "hall":
+        sc = scene.hall_scene(resolution=(W, H))
+    else:
+        sc = scene.soup_scene(n_tris=args.tris, resolution=(W, H))
+    cs = scene.compile_scene(sc)
     ctxs = []
     t0 = time.time()
     base = capi.HipContext(0)
