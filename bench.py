@@ -150,6 +150,8 @@ def time_split(pp, counts):
            "lanes": {"traversal_busy": round((cl["visits"] + sh["visits"]) / max(1, cl["slots_traversal"]), 4),
                      "triangle_loop": round((cl["tri_tests"] + sh["tri_tests"]) / max(1, cl["slots_tri"]), 4)},
            "iterations_per_wave": round(pp["trav_iters"] / max(1, pp["waves"]), 1),
+           # the launch lasts as long as its longest wave: the ratio to the mean wave is the launch's tail
+           "longest_wave_over_mean": round(pp["t_max"] * pp["waves"] / tot, 4) if pp.get("waves") else None,
            "source": "counting build, untimed 1-spp pass; wave-uniform wall clocks (100 MHz) around an explicit "
                      "vmcnt(0) wait after each node / leaf load batch"}
     return out
