@@ -134,7 +134,7 @@ def main(tag):
         kernels[k] = rec
 
     out += ["", "## Per-launch counters (the timed launch for the persistent path kernel; mean per launch otherwise)", "",
-            "| kernel | VGPR | AGPR | SGPR | LDS B | scratch | grid | HBM read MB (2x FETCH) | WRITE_SIZE MB | "
+            "| kernel | VGPR | AGPR | SGPR | LDS B | scratch | grid | HBM read MB (128 B x requests, or 2x FETCH) | WRITE_SIZE MB | "
             "TCC_MISS x 128 B MB | L2 hit % | TCC_REQ x 128 B GB |", "|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for k, rec in kernels.items():
         c = rec["counters"]
