@@ -256,6 +256,7 @@ struct RaygenArgs {
     int32_t first_pass;
     uint4 *probe;                  // optional, per slot (akr_pixel_probe): .y counts the camera ray
     const uint32_t *order;         // optional: queue position -> slot (the cost order)
+    uint32_t slot_base;            // without `order`: queue position i holds slot slot_base + i
     uint32_t lookahead;            // nonzero: k_raygen_lanes over the planned lanes of `look`
     LookArgs look;
 };
@@ -265,6 +266,8 @@ struct SplatArgs {
     float4 *film;
     uint32_t n;
     float ray_clamp;
+    const uint32_t *order;         // optional: slot of entry i (a half's share of the cost order) ...
+    uint32_t slot_base;            // ... else slot_base + i
     uint32_t lookahead;            // nonzero: per active pixel of `look`, its accepted lanes in chain order
     LookArgs look;
 };

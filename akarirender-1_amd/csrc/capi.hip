@@ -351,6 +351,9 @@ struct akr_hip_ctx {
     // option "wave_order": the wavefront's camera rays queued in the cost order (costliest first in
     // each shard of the closest-hit launch), by the same rule and floors as the persistent kernels
     bool wave_order = true;
+    // option "wave_dual": the wavefront as two half-frame pipelines, one per internal stream (A/B
+    // option)
+    bool wave_dual = false;
     DBuf<uint4> d_pprobe;  // the path pilot's per-slot probe
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -898,7 +901,7 @@ struct akr_hip_ctx {
         if (cur_slots >= (1ull << 31)) throw std::runtime_error("lookahead slot budget too large");
         serialize(st);
         ensure_capacity(cur_slots);  // before any upload: a reallocation drops contents
-        d_counts.reserve(2 * n_count_words);
+        d_counts.reserve(4 * n_count_words);  // two pass parities (x two half-frame pipelines, option wave_dual)
         n_pix_last = N;
         if (N == 0) return 0;
         ensure_side_stream();
@@ -1210,6 +1213,96 @@ struct akr_hip_ctx {
                 worder = d_oidx[1].p;
             }
             last_ordered = worder ? 1 : 0;
+        }
+        // Two half-frame pipelines (option "wave_dual"): the slots split into two halves
+        // (two contiguous ranges of the queue order), each running its whole bounce chain — raygen,
+        // then per bounce closest-hit trace, shade, shadow trace, and the splat — on its own stream
+        // (half 0 on the main stream, half 1 on the side stream), so one half's kernels fill the CUs
+        // while the other half's trace launch drains.  The halves share nothing but the slot-indexed
+        // arrays, whose slots they split; each pixel's samples stay in order on its stream.
+        if (wave_dual && !la && p.spp > 0 && N >= 2 * (uint64_t)kTraceBlock) {
+            const uint32_t half[2] = {(uint32_t)(N / 2), (uint32_t)(N - N / 2)}, base[2] = {0, (uint32_t)(N / 2)};
+            hipStream_t hs[2] = {ms, side};
+            HIPCHK(hipEventRecord(ev_shade[0], ms));  // the side stream starts after the pilot's order
+            HIPCHK(hipStreamWaitEvent(side, ev_shade[0], 0));
+            DBuf<uint2> *ovf[2] = {&d_ovf, &d_ovf_side};
+            for (int s = 0; s < p.spp; s++) {
+                const int ps = s & 1;
+                last_passes++;
+                float4 *L = d_L[ps].p;
+                for (int h = 0; h < 2; h++) {
+                    hipStream_t hst = hs[h];
+                    const size_t bs = base[h];
+                    uint32_t *cnt = d_counts.p + (size_t)(2 * h + ps) * n_count_words;
+                    auto qcount = [&](int b) { return cnt + (size_t)b * kWorkStride; };
+                    auto scount = [&](int b) { return cnt + (size_t)(D + b) * kWorkStride; };
+                    auto work = [&](int b, int k) { return cnt + 2 * (size_t)D * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
+                    HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), hst));
+                    RaygenArgs rg = raygen_args(half[h], L, qcount(0), s == 0);
+                    rg.ray_out = d_ray0.p + 2 * bs;
+                    rg.state_out = d_state0.p + bs;
+                    rg.slot_out = d_slot0.p + bs;
+                    rg.probe = probe_p;
+                    rg.order = worder ? worder + bs : nullptr;
+                    rg.slot_base = (uint32_t)bs;
+                    timed("raygen", hst, [&] { launch_raygen(rg, hst); });
+                    for (int b = 0; b < nb; b++) {
+                        const bool odd = b & 1;
+                        TraceArgs t = trace_args(work(b, 0));
+                        t.rays = (odd ? d_ray1.p : d_ray0.p) + 2 * bs;
+                        t.count = qcount(b);
+                        t.hits = d_hit.p + bs;
+                        t.stack_ovf = ovf[h]->p;
+                        timed("trace_closest", hst, [&] { trace_launch(TRACE_CLOSEST, tight, t, half[h], hst); });
+                        ShadeArgs sh{};
+                        sh.sc = sd;
+                        sh.ray_in = (odd ? d_ray1.p : d_ray0.p) + 2 * bs;
+                        sh.state_in = (odd ? d_state1.p : d_state0.p) + bs;
+                        sh.slot_in = (odd ? d_slot1.p : d_slot0.p) + bs;
+                        sh.hit_in = d_hit.p + bs;
+                        sh.count_in = qcount(b);
+                        sh.ray_out = (odd ? d_ray0.p : d_ray1.p) + 2 * bs;
+                        sh.state_out = (odd ? d_state0.p : d_state1.p) + bs;
+                        sh.slot_out = (odd ? d_slot0.p : d_slot1.p) + bs;
+                        sh.count_out = qcount(b + 1);
+                        sh.shadow_ray = d_sray[0].p + 2 * bs;
+                        sh.shadow_color = d_scolor[0].p + bs;
+                        sh.shadow_count = scount(b);
+                        sh.seed = d_seed.p;
+                        sh.L = L;
+                        sh.depth = b;
+                        sh.max_depth = p.max_depth;
+                        sh.last = b == nb - 1;
+                        sh.probe = probe_p;
+                        timed("shade", hst, [&] { launch_shade(sh, half[h], hst); });
+                        if (b < p.max_depth) {
+                            TraceArgs ts = trace_args(work(b, 1));
+                            ts.stack_ovf = ovf[h]->p;  // the half's own stream: after its closest-hit trace
+                            ts.rays = d_sray[0].p + 2 * bs;
+                            ts.count = scount(b);
+                            ts.shadow_color = d_scolor[0].p + bs;
+                            ts.L = L;
+                            timed("trace_shadow", hst, [&] { trace_launch(TRACE_SHADOW, tight, ts, half[h], hst); });
+                        }
+                    }
+                    SplatArgs sp{};
+                    sp.L = L;
+                    sp.film = d_film.p;
+                    sp.n = half[h];
+                    sp.order = worder ? worder + bs : nullptr;
+                    sp.slot_base = (uint32_t)bs;
+                    sp.ray_clamp = p.ray_clamp;
+                    timed("splat", hst, [&] { launch_splat(sp, half[h], hst); });
+                }
+            }
+            last_form = AKR_FORM_WAVEFRONT;
+            if (probe_p) {
+                HIPCHK(hipEventRecord(ev_splat[0], side));
+                HIPCHK(hipStreamWaitEvent(ms, ev_splat[0], 0));
+                launch_probe_seed(d_seed.p, (uint32_t)N, probe_p, ms);
+            }
+            join_streams(st);
+            return N;
         }
         for (int s = 0; s < p.spp; s++) {
             const int ps = s & 1;
@@ -1556,6 +1649,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_tail_ppl10") {
             if (value < 0) throw std::runtime_error("path_tail_ppl10 must be >= 0");
             ctx->path_tail_ppl10 = value;
+        } else if (k == "wave_dual") {
+            ctx->wave_dual = value != 0;
         } else if (k == "leaf_align") {
             if (value != 1 && value != 2 && value != 4 && value != 8) throw std::runtime_error("leaf_align must be 1, 2, 4 or 8");
             ctx->leaf_align = (int)value;

@@ -831,7 +831,7 @@ __global__ __launch_bounds__(kBlock) void k_raygen(RaygenArgs a) {
     if (i >= a.n) return;
     // queue entry i holds slot sl: with the cost order the costliest camera rays are fetched first
     // in each XCD shard of the closest-hit launch (the order's shards are the launch's shards)
-    const uint32_t sl = a.order ? a.order[i] : i;
+    const uint32_t sl = a.order ? a.order[i] : a.slot_base + i;
     const uint32_t px = a.pixel[sl];
     const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
     uint32_t seed = a.first_pass ? (uint32_t)(x + y * a.cam.width) : a.seed[sl];
@@ -1448,9 +1448,10 @@ __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
         return;
     }
     if (i >= a.n) return;
-    float4 f = a.film[i];
-    splat_one(f, a.L[i], a.ray_clamp);
-    a.film[i] = f;
+    const uint32_t sl = a.order ? a.order[i] : a.slot_base + i;
+    float4 f = a.film[sl];
+    splat_one(f, a.L[sl], a.ray_clamp);
+    a.film[sl] = f;
 }
 
 // ------------------------------------------------------------------------------ persistent path

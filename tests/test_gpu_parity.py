@@ -778,3 +778,24 @@ def test_cornell_gpu_render_matches_reference_ref_png(hip_ctx_factory, spp):
           f"gap blocks darker: {gap_darker}/10")
     assert frac >= 0.99, fails
     assert gap_darker >= 8
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_wavefront_dual_pipelines_bit_exact(hip_ctx_factory, order):
+    """The wavefront as two half-frame pipelines (option wave_dual, DESIGN.md §0: each half's raygen,
+    closest-hit / shade / shadow launches and splat on its own stream) renders the oracle's image bit
+    for bit, final sampler states and per-pixel ray counts included: Glossy / Mix, image textures and
+    a 100K soup, depths 0-5, ragged and overlapping tiles, with and without the cost-ordered camera
+    rays (order 1 forces the order at every spp)."""
+    for sc, W, H in ((mixed_scene((48, 48)), 48, 48), (textured_scene((48, 48)), 48, 48),
+                     (small_soup(100_000, (96, 54)), 96, 54)):
+        with hip_ctx_factory(0) as ctx:
+            cs, orc = _setup(ctx, sc)
+            ctx.set_option("path", 0)
+            ctx.set_option("wave_dual", 1)
+            ctx.set_option("path_order_min_spp", 0 if order else 10 ** 6)
+            ctx.set_option("path_order_share_min_spp", 0 if order else 10 ** 6)
+            tiles = [(0, 0, W, H), (5, 3, W - 7, H - 9), (W // 2, 0, W, H // 3)]
+            for spp, depth in ((3, 5), (2, 0), (2, 1), (4, 2)):
+                _check_render(ctx, orc, spp, depth, tiles, W, H, probe=True)
+                assert ctx.render_form() == {"form": "wavefront", "ordered": bool(order)}
