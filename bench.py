@@ -782,8 +782,11 @@ def main():
         side_kw = dict(build_kw)
         configs = {}
         for name in SIDE_LEGS:
-            configs[name] = side_leg(name, local, args.max_depth, args.tile, side_kw,
-                                     lambda d: torch.cuda.current_stream(d).cuda_stream)
+            try:   # a side leg never costs the headline line
+                configs[name] = side_leg(name, local, args.max_depth, args.tile, side_kw,
+                                         lambda d: torch.cuda.current_stream(d).cuda_stream)
+            except Exception as e:  # noqa: BLE001  (reported in the line, not raised)
+                configs[name] = {"error": f"{type(e).__name__}: {e}"}
             log(f"[rank 0] side leg {name}: {configs[name]}")
 
     line = {
