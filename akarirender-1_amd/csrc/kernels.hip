@@ -139,6 +139,35 @@ __device__ __forceinline__ bool is_leaf(uint32_t c) { return (c & AKR_CHILD_LEAF
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 typedef __attribute__((address_space(1))) unsigned long long glb_u64;
 
+// An LDS stack entry.  A/B build AKR_STACK16: the ref in a u32 array and the entry distance's top
+// 16 bits (a positive float truncated: never above the exact distance, so a pop culls no entry the
+// exact value would keep, and only the order-free extra visits of a few near-ties are added) in a
+// u16 array behind it: 6 B per entry, so 15 entries and the park area fit 32 KB per workgroup.
+#ifdef AKR_STACK16
+typedef __attribute__((address_space(3))) uint32_t lds_u32s;
+typedef __attribute__((address_space(3))) unsigned short lds_u16s;
+constexpr int kStackLdsU64 = (kStackLds * kTraceBlock * 6 + 7) / 8;
+__device__ __forceinline__ unsigned long long lds_get(const lds_u64 *s, int e, uint32_t tid) {
+    const lds_u32s *r = (const lds_u32s *)s;
+    const lds_u16s *t = (const lds_u16s *)(r + kStackLds * kTraceBlock);
+    return (unsigned long long)r[e * kTraceBlock + tid] | ((unsigned long long)t[e * kTraceBlock + tid] << 48);
+}
+__device__ __forceinline__ void lds_put(lds_u64 *s, int e, uint32_t tid, unsigned long long v) {
+    lds_u32s *r = (lds_u32s *)s;
+    lds_u16s *t = (lds_u16s *)(r + kStackLds * kTraceBlock);
+    r[e * kTraceBlock + tid] = (uint32_t)v;
+    t[e * kTraceBlock + tid] = (unsigned short)(v >> 48);
+}
+#else
+constexpr int kStackLdsU64 = kStackLds * kTraceBlock;
+__device__ __forceinline__ unsigned long long lds_get(const lds_u64 *s, int e, uint32_t tid) {
+    return s[e * kTraceBlock + tid];
+}
+__device__ __forceinline__ void lds_put(lds_u64 *s, int e, uint32_t tid, unsigned long long v) {
+    s[e * kTraceBlock + tid] = v;
+}
+#endif
+
 
 // Pop the next stacked node whose stored entry distance is not beyond `lim` (the reference
 // re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
@@ -146,8 +175,8 @@ __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_
                                               uint32_t tid, uint32_t gtid, int &sp, float lim) {
 #ifdef AKR_POP2  // A/B build: the top two LDS entries in one ds_read2st64 (one round trip for a culled top)
     while (sp >= 2 && sp <= kStackLds) {
-        const unsigned long long e1 = s_stack[(sp - 1) * kTraceBlock + tid];
-        const unsigned long long e2 = s_stack[(sp - 2) * kTraceBlock + tid];
+        const unsigned long long e1 = lds_get(s_stack, sp - 1, tid);
+        const unsigned long long e2 = lds_get(s_stack, sp - 2, tid);
         if (!(__uint_as_float((uint32_t)(e1 >> 32)) > lim)) {
             sp -= 1;
             return (uint32_t)e1;
@@ -159,7 +188,7 @@ __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_
     while (sp > 0) {
         --sp;
         unsigned long long e;
-        if (sp < kStackLds) e = s_stack[sp * kTraceBlock + tid];
+        if (sp < kStackLds) e = lds_get(s_stack, sp, tid);
         else e = ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid];
         if (!(__uint_as_float((uint32_t)(e >> 32)) > lim)) return (uint32_t)e;
     }
@@ -206,7 +235,7 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
     const float tf = left_first ? t1 : t0;
     if (pn && pf) {
         const unsigned long long e = (unsigned long long)far_ref | ((unsigned long long)__float_as_uint(tf) << 32);
-        if (sp < kStackLds) s_stack[sp * kTraceBlock + tid] = e;
+        if (sp < kStackLds) lds_put(s_stack, sp, tid, e);
         else ovf[(size_t)(sp - kStackLds) * ovf_threads + gtid] = e;
         sp++;
     }
@@ -252,7 +281,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t order_lo, uint32_t orde
         for (int k = 0; k < 4; k++) {
             const bool push = (rest >> pos[k]) & 1u;
             const int e = sp + (push ? (int)__popc(rest >> (pos[k] + 1u)) : 3);
-            s_stack[e * kTraceBlock + tid] = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
+            lds_put(s_stack, e, tid, (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32));
         }
     } else {
 #pragma unroll
@@ -260,7 +289,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t order_lo, uint32_t orde
             if ((rest >> pos[k]) & 1u) {
                 const int e = sp + (int)__popc(rest >> (pos[k] + 1u));
                 const unsigned long long v = (unsigned long long)ref[k] | ((unsigned long long)__float_as_uint(t[k]) << 32);
-                if (e < kStackLds) s_stack[e * kTraceBlock + tid] = v;
+                if (e < kStackLds) lds_put(s_stack, e, tid, v);
                 else ovf[(size_t)(e - kStackLds) * ovf_threads + gtid] = v;
             }
         }
@@ -536,7 +565,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
     constexpr bool ANY = MODE == TRACE_ANY || MODE == TRACE_SHADOW;  // occlusion query: any hit in (tmin, tmax)
     // the pilot's steps-only build (TRACE_PILOT) counts steps without the counting build's tallies
     constexpr bool STEPS = COUNT || MODE == TRACE_PILOT;
-    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
@@ -1844,7 +1873,7 @@ constexpr int kParkSlots = 8;
 template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path(PathArgs pa) {
     const TraceArgs &a = pa.t;
-    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
     __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
@@ -2116,7 +2145,7 @@ struct DeferState {
 template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_defer(PathArgs pa) {
     const TraceArgs &a = pa.t;
-    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
     __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
     __shared__ uint32_t s_res[kTraceBlock];  // per owner lane: resolved bit (slot), occluded bit (16 + slot)
@@ -2467,7 +2496,7 @@ struct SpecState {
 template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_spec(PathArgs pa) {
     const TraceArgs &a = pa.t;
-    __shared__ unsigned long long s_stack_mem[kStackLds * kTraceBlock];
+    __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
     __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;

@@ -45,7 +45,7 @@ def worker(args):
         ctx.render_device(args.spp, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
         torch.cuda.synchronize(dev)
         out[name] = round((time.perf_counter() - t) / args.spp * 1e3, 4)
-        out[name + " form"] = ctx.render_form()["form"]
+        out[name + " form"] = ctx.render_form()["form"] + " ppl %.2f" % ctx.render_form_inputs()["pixels_per_lane"]
     ctx.close()
     print("RESULT " + json.dumps(out), flush=True)
 
