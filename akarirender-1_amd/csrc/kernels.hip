@@ -251,6 +251,10 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
 __device__ __forceinline__ float ubyte(uint32_t w, int k) {  // v_cvt_f32_ubyte{k}
     return (float)((w >> (8 * k)) & 0xFFu);
 }
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, float b, float c) {  // v_pk_fma_f32: fmaf per element
+    return __builtin_elementwise_fma(a, f2{b, b}, f2{c, c});
+}
 
 // Continue with the first entered slot of a wide node in the BVH2 depth-first order and push the
 // other entered slots behind it, each with its entry distance; pop when no slot is entered.
@@ -404,11 +408,28 @@ __device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t
     float t[4];
     bool hit[4];
     uint32_t ref[4] = {c.x, c.y, c.z, c.w};
+#ifdef AKR_PK_FMA  // A/B build: the slot bounds two slots at a time (v_pk_fma_f32, the same fma per element)
+    f2 pnx[2], pfx[2], pny[2], pfy[2], pnz[2], pfz[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        pnx[j] = pk_fma(f2{ubyte(qnx, 2 * j), ubyte(qnx, 2 * j + 1)}, scx, nox);
+        pfx[j] = pk_fma(f2{ubyte(qfx, 2 * j), ubyte(qfx, 2 * j + 1)}, scx, fox);
+        pny[j] = pk_fma(f2{ubyte(qny, 2 * j), ubyte(qny, 2 * j + 1)}, scy, noy);
+        pfy[j] = pk_fma(f2{ubyte(qfy, 2 * j), ubyte(qfy, 2 * j + 1)}, scy, foy);
+        pnz[j] = pk_fma(f2{ubyte(qnz, 2 * j), ubyte(qnz, 2 * j + 1)}, scz, noz);
+        pfz[j] = pk_fma(f2{ubyte(qfz, 2 * j), ubyte(qfz, 2 * j + 1)}, scz, foz);
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < 4; k++) {
+#ifdef AKR_PK_FMA
+        const float nx = pnx[k >> 1][k & 1], fx = pfx[k >> 1][k & 1], ny = pny[k >> 1][k & 1], fy = pfy[k >> 1][k & 1],
+                    nz = pnz[k >> 1][k & 1], fz = pfz[k >> 1][k & 1];
+#else
         const float nx = __builtin_fmaf(ubyte(qnx, k), scx, nox), fx = __builtin_fmaf(ubyte(qfx, k), scx, fox);
         const float ny = __builtin_fmaf(ubyte(qny, k), scy, noy), fy = __builtin_fmaf(ubyte(qfy, k), scy, foy);
         const float nz = __builtin_fmaf(ubyte(qnz, k), scz, noz), fz = __builtin_fmaf(ubyte(qfz, k), scz, foz);
+#endif
         const float tk = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
         const float m1 = fminf(fminf(fx, fy), fminf(fz, lim));
         t[k] = tk;
