@@ -1238,6 +1238,11 @@ __device__ __forceinline__ void shade_hit_tab(const SceneDev &s, const Tab &tab,
                                               V3 beta, uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
     o.emit = o.ext = o.sh = false;
     const ShadeTri tr = s.tri[gid];
+    // the whole record in one round trip: without this the compiler loads the material id alone, tests
+    // it, then loads the rest (two dependent trips; whole frame -0.6 %, profiles/r21_shade_trip_ab.log)
+    asm volatile("" ::"v"(tr.a.x), "v"(tr.a.y), "v"(tr.a.z), "v"(tr.a.w), "v"(tr.b.x), "v"(tr.b.y), "v"(tr.b.z),
+                 "v"(tr.b.w), "v"(tr.c.x), "v"(tr.c.y), "v"(tr.c.z), "v"(tr.c.w), "v"(tr.d.x), "v"(tr.d.y), "v"(tr.d.z),
+                 "v"(tr.d.w), "v"(tr.e.x), "v"(tr.e.y), "v"(tr.e.z));
     const int32_t mid = (int32_t)fbits(tr.a.w);
     if (mid < 0) return;  // a null material ends the path (undefined in the reference)
     const V3 v0{tr.a.x, tr.a.y, tr.a.z}, v1{tr.b.x, tr.b.y, tr.b.z}, v2{tr.c.x, tr.c.y, tr.c.z};
@@ -1700,9 +1705,27 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
 // others are traced inline with the exact BVH2 walk and come back finished (false).  An occlusion
 // ray's best starts at tmax (§3.8).  A return value, not bool references: a reference to one of two
 // flags picked per lane puts both in scratch.
+// The root node's box (the BVH2 root's, as path_begin tests it): A/B build AKR_ROOT_SGPR loads it once
+// per wave into wave-uniform registers instead of once per fresh ray
+struct RootBox {
+    float v[6];
+};
+__device__ __forceinline__ RootBox root_box(const TraceArgs &a) {
+    RootBox b{};
+#ifdef AKR_ROOT_SGPR
+    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
+    const float4 r0 = nodesf[0], r2 = nodesf[2];
+    const float w[6] = {r0.x, r0.y, r0.z, r0.w, r2.x, r2.y};
+#pragma unroll
+    for (int k = 0; k < 6; k++) b.v[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(w[k])));
+#endif
+    return b;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ bool path_begin(const TraceArgs &a, bool occl, float4 ra, float4 rb, PathRay &r,
-                                           lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid, PathCount &c) {
+                                           lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid, PathCount &c,
+                                           const RootBox &rbx) {
     r.o = V3{ra.x, ra.y, ra.z};
     r.d = V3{rb.x, rb.y, rb.z};
     r.tmin = ra.w;
@@ -1731,9 +1754,15 @@ __device__ __forceinline__ bool path_begin(const TraceArgs &a, bool occl, float4
         c.box[occl]++;
         c.deep_now = false;
     }
+#ifdef AKR_ROOT_SGPR
+    const float tr = box_test<true, true>(rbx.v[0], rbx.v[1], rbx.v[2], rbx.v[3], rbx.v[4], rbx.v[5], r.o, r.invd, r.tmin,
+                                          r.tmax);
+#else
+    (void)rbx;
     const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const float tr = box_test<true, true>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, r.o, r.invd, r.tmin, r.tmax);
+#endif
     r.cur = (a.wide_root == AKR_CHILD_EMPTY || tr < 0.0f || tr > r.best) ? AKR_CHILD_EMPTY : a.wide_root;
     return true;
 }
@@ -1905,6 +1934,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
+    const RootBox rbx = root_box(a);
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -2064,7 +2094,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     pc_closest += any ? 0u : 1u;
                     pc_shadow += any ? 1u : 0u;
                 }
-                busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
+                busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
                 fin = !busy;
             }
         }
@@ -2180,6 +2210,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
+    const RootBox rbx = root_box(a);
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -2420,7 +2451,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             path_unpark(s_park, tid, r, ff, kind_now == RAY_OWN_SHADOW || kind_now == RAY_FOREIGN);
             if (fresh) {
                 if (COUNT) pc_closest += occl ? 0u : 1u;  // own extension / camera rays
-                busy = path_begin<COUNT>(a, occl, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
+                busy = path_begin<COUNT>(a, occl, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
                 fin = !busy;
             }
         }
@@ -2535,6 +2566,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const uint32_t spp = pa.spp;
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
+    const RootBox rbx = root_box(a);
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -2835,7 +2867,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     sc_closest += next_any ? 0u : 1u;
                     sc_shadow += next_any ? 1u : 0u;
                 }
-                busy = path_begin<COUNT>(a, next_any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
+                busy = path_begin<COUNT>(a, next_any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
                 fin = !busy;
             }
         }
