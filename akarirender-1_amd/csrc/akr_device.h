@@ -38,13 +38,6 @@ constexpr int kTraceBlock = AKR_TRACE_BLOCK;  // threads per traversal workgroup
 #define AKR_REFILL_MIN 32
 #endif
 constexpr int kStackLds = AKR_STACK_LDS;  // LDS-resident traversal stack entries per ray (8 B each; 15 fill the LDS left by the path kernels' park area)
-// Wide nodes the persistent path kernels (k_path, k_path_spec) keep in LDS: the device copy of the wide
-// view puts the kTopLds nodes of largest area first (capi.hip top_nodes_first), and a visit of node
-// i < kTopLds reads it from LDS instead of through the vector memory pipe
-#ifndef AKR_TOP_LDS
-#define AKR_TOP_LDS 0
-#endif
-constexpr uint32_t kTopLds = AKR_TOP_LDS;
 constexpr int kStackMax = 96;         // >= 3 pushes x 32 wide levels (BVH2 depth <= 64)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kRefillMin = AKR_REFILL_MIN;  // refill a wave's idle lanes once at least this many are idle

@@ -9,8 +9,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <queue>
-#include <limits>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -1809,51 +1807,6 @@ void check_tris_match_mesh(const akr_hip_ctx *ctx, const akr_bvh_tri *tr, uint64
             throw std::runtime_error("imported BVH: scene triangle " + std::to_string(g) + " is in no leaf");
 }
 
-// The persistent path kernels keep the first kTopLds wide nodes in LDS (kernels.hip wide_load_top):
-// renumber the device copy so that those are the kTopLds nodes of largest box area, a top subtree
-// (a child's box lies inside its parent's, so each pick's parent was picked before it), root first,
-// the others after them in their depth-first order.  Child references are rewritten; leaf references
-// and the per-node order words (slot positions) do not change, so every traversal visits the same
-// nodes in the same order.
-void top_nodes_first(std::vector<akr_bvh4_node> &wn, uint32_t k) {
-    const uint32_t n = (uint32_t)wn.size();
-    k = std::min(k, n);
-    auto slot_area = [&](const akr_bvh4_node &nd, int s) {
-        double e[3];
-        for (int a = 0; a < 3; a++) {
-            const float step = std::ldexp(1.0f, (int)((nd.meta >> (8 * a)) & 0xFFu) - 127);
-            const uint32_t lo = (nd.q[2 * a] >> (8 * s)) & 0xFFu, hi = (nd.q[2 * a + 1] >> (8 * s)) & 0xFFu;
-            e[a] = std::max(0.0, ((double)hi - (double)lo) * step);
-        }
-        return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
-    };
-    std::vector<uint32_t> pick;
-    std::priority_queue<std::pair<double, uint32_t>> q;
-    q.push({std::numeric_limits<double>::infinity(), 0u});
-    while (!q.empty() && pick.size() < k) {
-        const uint32_t i = q.top().second;
-        q.pop();
-        pick.push_back(i);
-        for (int s = 0; s < 4; s++) {
-            const uint32_t c = wn[i].child[s];
-            if (c != AKR_CHILD_EMPTY && !(c & AKR_CHILD_LEAF)) q.push({slot_area(wn[i], s), c});
-        }
-    }
-    std::vector<uint32_t> perm(n, UINT32_MAX);
-    for (uint32_t j = 0; j < (uint32_t)pick.size(); j++) perm[pick[j]] = j;
-    uint32_t next = (uint32_t)pick.size();
-    for (uint32_t i = 0; i < n; i++)
-        if (perm[i] == UINT32_MAX) perm[i] = next++;
-    std::vector<akr_bvh4_node> out(n);
-    for (uint32_t i = 0; i < n; i++) {
-        akr_bvh4_node nd = wn[i];
-        for (auto &c : nd.child)
-            if (c != AKR_CHILD_EMPTY && !(c & AKR_CHILD_LEAF)) c = perm[c];
-        out[perm[i]] = nd;
-    }
-    wn.swap(out);
-}
-
 // After the BVH2 of ctx->bvh exists (built or imported): the wide view, its device copy, the BVH2
 // itself for the exact lane path, the accel info, and the scene's shading records.
 void finish_accel(akr_hip_ctx *ctx, int n_threads) {
@@ -1917,9 +1870,7 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         };
         run_on_threads(nt, fill);
         ctx->wide_root_dev = remap(ctx->bvh4.root_ref);
-        if (kTopLds > 0 && ctx->bvh4.root_ref == 0 && wn.size() > 1) top_nodes_first(wn, kTopLds);
-        ctx->d_wnodes.reserve(std::max<size_t>(1, kTopLds));  // never a null pointer; the LDS copy of the
-                                                               // first kTopLds nodes never reads past it
+        ctx->d_wnodes.reserve(1);  // never a null pointer, even for an empty scene
         ctx->d_wleaves.reserve(1);
         ctx->d_wnodes.upload(wn.data(), wn.size(), ctx->stream);
         ctx->d_wleaves.upload(blob.get(), words + pad, ctx->stream);

@@ -371,31 +371,6 @@ __device__ __forceinline__ WideNode wide_load(const float4 *wn, uint32_t cur) {
     return nd;
 }
 
-// A wide node from the LDS copy of the first kTopLds nodes (TOP: the kernel holds one) or through
-// the vector memory pipe
-typedef __attribute__((address_space(3))) uint32_t lds_u4;  // 16 words per node, read as 16-B vectors
-template <bool TOP>
-__device__ __forceinline__ WideNode wide_load_top(const float4 *wn, const lds_u4 *top, uint32_t cur) {
-    if constexpr (TOP) {
-        if (cur < kTopLds) {
-            const lds_u4 *t = top + 16 * cur;
-            WideNode nd;
-            nd.h = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]), __uint_as_float(t[3]));
-            nd.c = make_uint4(t[4], t[5], t[6], t[7]);
-            nd.qa = make_uint4(t[8], t[9], t[10], t[11]);
-            nd.qb = make_uint4(t[12], t[13], t[14], t[15]);
-            return nd;
-        }
-    }
-    return wide_load(wn, cur);
-}
-// The kernel's LDS copy of the first kTopLds wide nodes (one workgroup barrier)
-__device__ __forceinline__ void load_top(const float4 *wn, lds_u4 *top, uint32_t tid) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(wn);
-    for (uint32_t i = tid; i < 16 * kTopLds; i += kTraceBlock) top[i] = w[i];
-    __syncthreads();
-}
-
 template <bool ANY>
 __device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t &cur, V3 o, uint32_t dpos, V3 invd,
                                                     float tmin, float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
@@ -1582,10 +1557,10 @@ struct PathCount {
 // PRIO (k_path_spec, A/B build AKR_SPEC_PRIO): lanes running a speculative sample (`lowp`) do not
 // hold the wave in the loop while a committed-path lane is busy: the early exit counts only the
 // others' searching lanes.
-template <bool COUNT, bool PRIO = false, bool TOP = false>
+template <bool COUNT, bool PRIO = false>
 __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, const float4 *wn, lds_u64 *s_stack,
                                               glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
-                                              PathCount &c, const lds_u4 *top = nullptr, bool lowp = false) {
+                                              PathCount &c, bool lowp = false) {
     bool counted = true;  // this lane's search counts for the early exit
     if constexpr (PRIO) counted = !lowp || __ballot(busy && !lowp) == 0;
     while (true) {
@@ -1599,7 +1574,7 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
             const unsigned long long ta = wall_clock64();
             // every lane loads (an idle lane node 0, a cache hit): a load under a branch makes the
             // compiler wait for it inside the branch, before the clock below
-            const WideNode nd = wide_load_top<TOP>(wn, top, vis ? r.cur : 0u);
+            const WideNode nd = wide_load(wn, vis ? r.cur : 0u);
             const unsigned long long tb = wall_clock64();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             tc = wall_clock64();
@@ -1613,14 +1588,8 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
                 c.deep_now = c.deep_now || r.sp > kStackLds;
             }
         } else if (busy && is_internal(r.cur)) {
-            if constexpr (TOP) {
-                const WideNode nd = wide_load_top<true>(wn, top, r.cur);
-                visit_wide_lean_node<false>(nd, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf,
-                                            ovf_threads, tid, gtid, r.sp);
-            } else {
-                visit_wide_lean<false>(wn, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf, ovf_threads,
-                                       tid, gtid, r.sp);
-            }
+            visit_wide_lean<false>(wn, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf, ovf_threads, tid,
+                                   gtid, r.sp);
         }
         if (busy && r.leaf == AKR_CHILD_EMPTY && is_leaf(r.cur)) {
             r.leaf = r.cur;  // postpone the leaf and keep descending
@@ -1957,9 +1926,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
     __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
-    __shared__ uint4 s_top_mem[kTopLds > 0 ? 4 * kTopLds : 1];  // 16-B aligned
-    lds_u4 *s_top = (lds_u4 *)s_top_mem;
-    if constexpr (kTopLds > 0) load_top(pa.t.wide_nodes, s_top, threadIdx.x);
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
@@ -2140,8 +2106,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         if (!__any(busy)) continue;
         // ---- B. traversal phase, C. leaf phase (k_trace's, shared with k_path_defer)
         const int kd = any ? 1 : 0;
-        path_traverse<COUNT, false, (kTopLds > 0)>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid,
-                                                   gtid, c, s_top);
+        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
         if (COUNT) {
             const unsigned long long t = wall_clock64();
             p_tt += t - p_t;
@@ -2586,9 +2551,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
     __shared__ uint4 s_tab[TAB ? kTabBytes / 16 : 1];
-    __shared__ uint4 s_top_mem[kTopLds > 0 ? 4 * kTopLds : 1];  // 16-B aligned
-    lds_u4 *s_top = (lds_u4 *)s_top_mem;
-    if constexpr (kTopLds > 0) load_top(pa.t.wide_nodes, s_top, threadIdx.x);
     lds_u64 *s_stack = (lds_u64 *)s_stack_mem;
     glb_u64 *stack_ovf = (glb_u64 *)a.stack_ovf;
     const uint32_t tid = threadIdx.x;
@@ -2927,11 +2889,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         // ---- B. traversal phase, C. leaf phase (k_trace's, shared with the other persistent kernels)
         const int kd = s.any() ? 1 : 0;
 #ifdef AKR_SPEC_PRIO
-        path_traverse<COUNT, true, (kTopLds > 0)>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid,
-                                                  gtid, c, s_top, s.node() != 0u);
+        path_traverse<COUNT, true>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c,
+                                   s.node() != 0u);
 #else
-        path_traverse<COUNT, false, (kTopLds > 0)>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid,
-                                                   gtid, c, s_top);
+        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
 #endif
         if (COUNT) {
             const unsigned long long t = wall_clock64();
