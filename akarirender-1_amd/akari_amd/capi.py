@@ -101,7 +101,7 @@ BUILDER_SAH, BUILDER_LBVH, BUILDER_SBVH = 0, 1, 2
 COLLAPSE_SAH, COLLAPSE_BALANCED = 0, 1   # akr_build_params::wide_collapse
 MAT_DIFFUSE, MAT_GLOSSY, MAT_EMISSIVE, MAT_MIX = 0, 1, 2, 3
 PROBE_SEED, PROBE_RAYS = 1, 2
-FORM_NAMES = {-1: None, 0: "wavefront", 1: "wavefront+lookahead", 2: "k_path", 3: "k_path_defer", 4: "k_path_spec"}
+FORM_NAMES = {-1: None, 0: "wavefront", 1: "wavefront+lookahead", 2: "k_path", 3: "k_path_defer", 4: "k_path_spec", 5: "wavefront_stream"}
 
 # numpy views of the POD structs (for vectorised ray/hit buffers)
 RAY_DTYPE = np.dtype([("o", np.float32, 3), ("tmin", np.float32), ("d", np.float32, 3), ("tmax", np.float32)])

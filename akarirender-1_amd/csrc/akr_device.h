@@ -184,6 +184,18 @@ struct ShadeArgs {
     int32_t depth;
     int32_t max_depth;
     int32_t last;                  // no extension ray is traced after this bounce
+    // streaming wavefront (option wave_stream): queue entries of every bounce depth and
+    // both sample parities in one launch; a finished sample goes to the splat queue and, while the
+    // slot has samples left, its next sample to the regeneration queue
+    const uint32_t *aux_in;        // per entry: depth | sample parity << 16 (nullptr: classic k_shade)
+    uint32_t *aux_out;
+    uint32_t *left;                // per slot: samples not yet started
+    uint32_t *regen;               // slot | parity << 31 of each sample to start
+    uint32_t *regen_count;
+    uint32_t *splat_q;             // slot | parity << 31 of each finished sample
+    uint32_t *splat_count;
+    uint32_t n_slots;              // L holds two parities of n_slots entries each
+    int32_t nb;                    // traced bounces per sample
 };
 
 // One AO bounce (cpu/integrator.cpp:46-56) for every queued camera hit: appends the AO ray to
@@ -259,10 +271,17 @@ struct RaygenArgs {
     uint32_t slot_base;            // without `order`: queue position i holds slot slot_base + i
     uint32_t lookahead;            // nonzero: k_raygen_lanes over the planned lanes of `look`
     LookArgs look;
+    // streaming wavefront: k_stream_start (every slot's first sample, `left` = spp - 1) and
+    // k_raygen_stream (the regeneration queue's samples appended to the ray queue)
+    uint32_t *left;
+    uint32_t *aux_out;
+    uint32_t spp;
+    const uint32_t *regen;
+    const uint32_t *regen_count;
 };
 
 struct SplatArgs {
-    const float4 *L;
+    float4 *L;
     float4 *film;
     uint32_t n;
     float ray_clamp;
@@ -270,6 +289,9 @@ struct SplatArgs {
     uint32_t slot_base;            // ... else slot_base + i
     uint32_t lookahead;            // nonzero: per active pixel of `look`, its accepted lanes in chain order
     LookArgs look;
+    const uint32_t *queue;         // streaming wavefront: finished samples (slot | parity << 31) ...
+    const uint32_t *queue_count;   // ... and their count; L holds two parities of n_slots entries
+    uint32_t n_slots;
 };
 
 // k_path counting build: per-wave phase profile (wall clock, 100 MHz), summed over waves

@@ -354,6 +354,16 @@ struct akr_hip_ctx {
     // option "wave_dual": the wavefront as two half-frame pipelines, one per internal stream (A/B
     // option)
     bool wave_dual = false;
+    // option "wave_stream": the streaming wavefront: one ray queue holding every
+    // active slot's current ray whatever its bounce, a finished sample's slot regenerated into the
+    // next launch, so every closest-hit launch carries about one ray per active slot instead of
+    // the shrinking queue of one bounce of one sample pass
+    bool wave_stream = false;
+    DBuf<float4> d_Ls;                          // two sample parities of per-slot radiance
+    DBuf<uint32_t> d_aux[2], d_left, d_regq, d_splq[2];
+    hipEvent_t ev_sm[4] = {}, ev_ss[4] = {}, ev_poll[8] = {};
+    uint32_t *h_spoll = nullptr, *d_spoll_host = nullptr;  // mapped: queue counts polled by the host
+    int64_t last_stream_iters = 0;
     DBuf<uint4> d_pprobe;  // the path pilot's per-slot probe
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -429,6 +439,13 @@ struct akr_hip_ctx {
         if (h_remain) (void)hipHostFree(h_remain);
         if (h_check) (void)hipHostFree(h_check);
         if (h_sum) (void)hipHostFree(h_sum);
+        if (h_spoll) (void)hipHostFree(h_spoll);
+        for (hipEvent_t e : ev_sm)
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_ss)
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_poll)
+            if (e) (void)hipEventDestroy(e);
         if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_gather) (void)hipEventDestroy(ev_gather);
@@ -1214,6 +1231,7 @@ struct akr_hip_ctx {
             }
             last_ordered = worder ? 1 : 0;
         }
+        if (wave_stream && !la && p.spp > 0) return render_stream(p, N, nb, tight, sd, probe_p, worder, st);
         // Two half-frame pipelines (option "wave_dual"): the slots split into two halves
         // (two contiguous ranges of the queue order), each running its whole bounce chain — raygen,
         // then per bounce closest-hit trace, shade, shadow trace, and the splat — on its own stream
@@ -1410,6 +1428,181 @@ struct akr_hip_ctx {
         }
         // the last shade of every pass ran on the main stream and left each slot's sampler state
         if (probe_p && p.spp > 0) launch_probe_seed(d_seed.p, (uint32_t)N, probe_p, ms);
+        join_streams(st);
+        return N;
+    }
+
+    // The streaming wavefront (option wave_stream).  Iteration i on the main stream: the closest-hit
+    // trace of the queue (every active slot's current ray: camera rays and extension rays of any
+    // bounce), k_shade over its hits (emission into the sample's L, the NEE shadow ray into shadow
+    // queue i % 2, the extension ray into the next queue; a path that ends queues its sample for
+    // the splat and, while the slot has samples left, the slot's next sample for regeneration), and
+    // k_raygen_stream (the regenerated samples' camera rays, behind the extension rays).  On the
+    // side stream: the shadow trace of queue i % 2 (adding to L when unoccluded) and the splat of
+    // the samples that ended in iteration i, whose last shadow result is then in.  A slot has one
+    // ray in flight, its samples start in order and each starts from the sampler state its
+    // predecessor ended with, so every sample, its L additions (emission, then the NEE results in
+    // bounce order) and the film sums are the sequential loop's (cpu/integrator.cpp:124-134).
+    // Per-iteration counters come from a ring of four blocks; a block, the shadow queue and the
+    // splat queue of iteration i are reused by iteration i + 4 / i + 2 only after the side stream is
+    // done with them (events).  The host polls the queue count every 16 iterations through mapped
+    // memory, staying at most 48 iterations ahead of the device, and stops when the queue is empty.
+    uint64_t render_stream(const akr_pt_params &p, uint64_t N, int nb, bool tight, const SceneDev &sd, uint4 *probe_p,
+                           const uint32_t *worder, hipStream_t st) {
+        hipStream_t ms = main_st;
+        const uint32_t n = (uint32_t)N;
+        d_Ls.reserve(2 * N);
+        for (int k = 0; k < 2; k++) {
+            d_aux[k].reserve(N);
+            d_splq[k].reserve(N);
+        }
+        d_left.reserve(N);
+        d_regq.reserve(N);
+        if (!ev_sm[0]) {
+            for (int k = 0; k < 4; k++) {
+                HIPCHK(hipEventCreateWithFlags(&ev_sm[k], hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&ev_ss[k], hipEventDisableTiming));
+            }
+            for (int k = 0; k < 8; k++) HIPCHK(hipEventCreateWithFlags(&ev_poll[k], hipEventDisableTiming));
+            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_spoll), 8 * sizeof(uint32_t),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_spoll_host), h_spoll, 0));
+        }
+        // ring block k: [queue count out | shadow count | regen count | splat count | 2 x trace work]
+        const size_t bw = 4 * (size_t)kWorkStride + 2 * (size_t)kTraceWords;
+        if (d_counts.n < 4 * bw) throw std::runtime_error("internal: stream counter ring");
+        auto blk = [&](int64_t i) { return d_counts.p + (size_t)(i & 3) * bw; };
+        auto qcnt = [&](int64_t i) { return blk(i); };
+        auto scnt = [&](int64_t i) { return blk(i) + kWorkStride; };
+        auto rcnt = [&](int64_t i) { return blk(i) + 2 * (size_t)kWorkStride; };
+        auto pcnt = [&](int64_t i) { return blk(i) + 3 * (size_t)kWorkStride; };
+        auto work = [&](int64_t i, int k) { return blk(i) + 4 * (size_t)kWorkStride + (size_t)k * kTraceWords; };
+        HIPCHK(hipMemsetAsync(d_counts.p, 0, 4 * bw * sizeof(uint32_t), ms));
+        {
+            RaygenArgs rg = raygen_args(n, d_Ls.p, qcnt(-1), true);  // iteration -1's queue: the first samples
+            rg.order = worder;
+            rg.probe = probe_p;
+            rg.left = d_left.p;
+            rg.aux_out = d_aux[0].p;
+            rg.spp = (uint32_t)p.spp;
+            timed("raygen", ms, [&] { launch_stream_start(rg, ms); });
+        }
+#ifdef AKR_STREAM_DEBUG  // debug build: every stage synchronised and checked, so a fault names its kernel
+        auto dbg = [&](const char *stage, int64_t it) {
+            const hipError_t e1 = hipStreamSynchronize(ms), e2 = hipStreamSynchronize(side);
+            if (e1 != hipSuccess || e2 != hipSuccess)
+                throw std::runtime_error(std::string("stream debug: ") + stage + " at iteration " + std::to_string(it) +
+                                         ": " + hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+        };
+#else
+        auto dbg = [](const char *, int64_t) {};
+#endif
+        dbg("start", -1);
+        const int64_t cap_iters = (int64_t)p.spp * nb + 1;  // the longest chain: spp samples of nb traced bounces
+        int64_t i = 0;
+        bool empty = false;
+        for (; i < cap_iters && !empty; i++) {
+            const int q = (int)(i & 1);
+            if (i >= 4) HIPCHK(hipStreamWaitEvent(ms, ev_ss[i & 3], 0));  // block i & 3 free (iteration i - 4)
+            HIPCHK(hipMemsetAsync(blk(i), 0, bw * sizeof(uint32_t), ms));
+            TraceArgs t = trace_args(work(i, 0));
+            t.rays = q ? d_ray1.p : d_ray0.p;
+            t.count = qcnt(i - 1);
+            t.hits = d_hit.p;
+            timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
+            dbg("trace_closest", i);
+            // shadow queue, splat queue and L parity of iteration i - 2 are done with on the side stream
+            if (i >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_ss[(i - 2) & 3], 0));
+            ShadeArgs sh{};
+            sh.sc = sd;
+            sh.ray_in = q ? d_ray1.p : d_ray0.p;
+            sh.state_in = q ? d_state1.p : d_state0.p;
+            sh.slot_in = q ? d_slot1.p : d_slot0.p;
+            sh.aux_in = d_aux[q].p;
+            sh.hit_in = d_hit.p;
+            sh.count_in = qcnt(i - 1);
+            sh.ray_out = q ? d_ray0.p : d_ray1.p;
+            sh.state_out = q ? d_state0.p : d_state1.p;
+            sh.slot_out = q ? d_slot0.p : d_slot1.p;
+            sh.aux_out = d_aux[q ^ 1].p;
+            sh.count_out = qcnt(i);
+            sh.shadow_ray = d_sray[q].p;
+            sh.shadow_color = d_scolor[q].p;
+            sh.shadow_count = scnt(i);
+            sh.seed = d_seed.p;
+            sh.L = d_Ls.p;
+            sh.max_depth = p.max_depth;
+            sh.nb = nb;
+            sh.n_slots = n;
+            sh.left = d_left.p;
+            sh.regen = d_regq.p;
+            sh.regen_count = rcnt(i);
+            sh.splat_q = d_splq[q].p;
+            sh.splat_count = pcnt(i);
+            sh.probe = probe_p;
+            timed("shade", ms, [&] { launch_shade(sh, n, ms); });
+            dbg("shade", i);
+            RaygenArgs rg = raygen_args(n, d_Ls.p, qcnt(i), false);
+            rg.ray_out = q ? d_ray0.p : d_ray1.p;
+            rg.state_out = q ? d_state0.p : d_state1.p;
+            rg.slot_out = q ? d_slot0.p : d_slot1.p;
+            rg.aux_out = d_aux[q ^ 1].p;
+            rg.regen = d_regq.p;
+            rg.regen_count = rcnt(i);
+            rg.probe = probe_p;
+            timed("raygen", ms, [&] { launch_raygen_stream(rg, n, ms); });
+            dbg("raygen", i);
+            const bool poll = (i & 15) == 15;
+            if (poll) {
+                reinterpret_cast<volatile uint32_t *>(h_spoll)[(i >> 4) & 7] = kMappedSentinel;
+                launch_store_word(qcnt(i), d_spoll_host + ((i >> 4) & 7), ms);
+            }
+            HIPCHK(hipEventRecord(ev_sm[i & 3], ms));
+            HIPCHK(hipStreamWaitEvent(side, ev_sm[i & 3], 0));
+            if (p.max_depth > 0) {
+                TraceArgs ts = trace_args(work(i, 1));
+                ts.stack_ovf = d_ovf_side.p;  // concurrent with the next iteration's main-stream trace
+                ts.rays = d_sray[q].p;
+                ts.count = scnt(i);
+                ts.shadow_color = d_scolor[q].p;
+                ts.L = d_Ls.p;
+                timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, side); });
+                dbg("trace_shadow", i);
+            }
+            SplatArgs sp{};
+            sp.L = d_Ls.p;
+            sp.film = d_film.p;
+            sp.n = n;
+            sp.ray_clamp = p.ray_clamp;
+            sp.queue = d_splq[q].p;
+            sp.queue_count = pcnt(i);
+            sp.n_slots = n;
+            timed("splat", side, [&] { launch_splat_stream(sp, n, side); });
+            dbg("splat", i);
+            HIPCHK(hipEventRecord(ev_ss[i & 3], side));
+            if (poll) {
+                HIPCHK(hipEventRecord(ev_poll[(i >> 4) & 7], ms));
+                // the poll two back (32 iterations earlier): wait for it, stop once its queue was empty
+                const int64_t k = (i >> 4) - 2;
+                if (k >= 0) {
+                    HIPCHK(hipEventSynchronize(ev_poll[k & 7]));
+                    const uint32_t c = read_mapped(h_spoll + (k & 7));
+                    if (c == kMappedSentinel) throw std::runtime_error("stream poll: the device never stored the count");
+                    if (c == 0) empty = true;
+                }
+            }
+        }
+        last_stream_iters = i;
+        last_passes = p.spp;
+        last_form = AKR_FORM_WAVE_STREAM;
+        if (!empty) {  // ran to the cap: the queue must be empty now (every chain is at most cap long)
+            HIPCHK(hipStreamSynchronize(ms));
+            reinterpret_cast<volatile uint32_t *>(h_spoll)[0] = kMappedSentinel;
+            launch_store_word(qcnt(i - 1), d_spoll_host, ms);
+            HIPCHK(hipStreamSynchronize(ms));
+            if (read_mapped(h_spoll) != 0) throw std::runtime_error("stream: rays left after the longest chain");
+        }
+        if (probe_p) launch_probe_seed(d_seed.p, n, probe_p, ms);  // every slot's final sampler state
         join_streams(st);
         return N;
     }
@@ -1651,6 +1844,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_tail_ppl10 = value;
         } else if (k == "wave_dual") {
             ctx->wave_dual = value != 0;
+        } else if (k == "wave_stream") {
+            ctx->wave_stream = value != 0;
         } else if (k == "leaf_align") {
             if (value != 1 && value != 2 && value != 4 && value != 8) throw std::runtime_error("leaf_align must be 1, 2, 4 or 8");
             ctx->leaf_align = (int)value;

@@ -14,6 +14,10 @@ int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st);
+// streaming wavefront (option wave_stream): first samples, regenerated samples, finished-sample splats
+void launch_stream_start(const RaygenArgs &a, hipStream_t st);
+void launch_raygen_stream(const RaygenArgs &a, uint32_t max_items, hipStream_t st);
+void launch_splat_stream(const SplatArgs &a, uint32_t max_items, hipStream_t st);
 void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st);
 void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st);
 void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st);

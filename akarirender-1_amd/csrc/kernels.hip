@@ -98,7 +98,8 @@ __device__ __forceinline__ uint32_t lane_prefix(unsigned long long m) {
 // workgroup (issued by two different waves, so the two round trips overlap).  A single counter
 // word sustains only ~88 returning atomics/us chip-wide (MI355X_MICROARCH.md, dequeue), so one
 // atomic per WAVE made the shade kernel atomic-bound; per workgroup it is 4x fewer.
-// Must be reached by every thread of the block.
+// Must be reached by every thread of the block; a second call in the same kernel needs a barrier
+// before it (the LDS words are the same).
 template <int BS = kBlock>
 __device__ __forceinline__ void block_append2(bool want_a, uint32_t *ctr_a, uint32_t &pos_a, bool want_b,
                                               uint32_t *ctr_b, uint32_t &pos_b) {
@@ -1367,39 +1368,63 @@ __device__ __noinline__ void shade_hit_call(const SceneDev s, uint32_t gid, floa
 #define AKR_SHADE_BLOCK 256
 #endif
 constexpr int kShadeBlock = AKR_SHADE_BLOCK;  // threads per shade workgroup (one queue atomic each)
-__global__ __launch_bounds__(kShadeBlock) void k_shade(ShadeArgs a) {
+// STREAM (the streaming wavefront, option wave_stream): every entry carries its bounce depth and its
+// sample's parity (two L buffers per slot, so a finished sample can wait for its last shadow result
+// while the slot's next sample accumulates); a sample whose path ends is queued for the splat and,
+// while the slot has samples left, its next sample for k_raygen_stream.  Each slot has exactly one
+// entry in flight, so the per-slot reads and writes below never race.
+template <bool STREAM>
+__global__ __launch_bounds__(kShadeBlock) void k_shade_t(ShadeArgs a) {
     const uint32_t i = blockIdx.x * kShadeBlock + threadIdx.x;
     const uint32_t n = *a.count_in;
     if (blockIdx.x * kShadeBlock >= n) return;  // whole workgroup past the queue (uniform: before any barrier)
     Bounce bo;
     bo.ext = bo.sh = false;
-    uint32_t slot = 0, seed = 0;
+    uint32_t slot = 0, seed = 0, aux = 0, li = 0;
+    bool ended = false, regen = false;
     if (i < n) {
         slot = a.slot_in[i];
+        li = slot;
+        int depth = a.depth;
+        bool last = a.last != 0;
+        if constexpr (STREAM) {
+            aux = a.aux_in[i];
+            depth = (int)(aux & 0xFFFFu);
+            last = depth == a.nb - 1;
+            li = slot + ((aux >> 16) & 1u) * a.n_slots;
+        }
         const float4 stv = a.state_in[i];
         seed = fbits(stv.w);
         const float4 hv = a.hit_in[i];
         const uint32_t gid = fbits(hv.w);
         if (gid != kNoHit) {  // miss -> on_miss (no-op), the path ends
             const float4 rdv = a.ray_in[2 * (size_t)i + 1];
-            shade_hit(a.sc, gid, hv.y, hv.z, neg(v3(rdv.x, rdv.y, rdv.z)), V3{stv.x, stv.y, stv.z}, seed, a.depth,
-                      a.max_depth, a.last != 0, bo);
+            shade_hit(a.sc, gid, hv.y, hv.z, neg(v3(rdv.x, rdv.y, rdv.z)), V3{stv.x, stv.y, stv.z}, seed, depth,
+                      a.max_depth, last, bo);
             if (bo.emit) {
-                float4 l = a.L[slot];
+                float4 l = a.L[li];
                 l.x += bo.e.x;
                 l.y += bo.e.y;
                 l.z += bo.e.z;
-                a.L[slot] = l;
+                a.L[li] = l;
             }
         }
         // the path does not reach another traced bounce: persist its sampler stream for the next
-        // sample pass (the stream continues across spp, cpu/integrator.cpp:124-134)
+        // sample (the stream continues across spp, cpu/integrator.cpp:124-134)
         if (!bo.ext) a.seed[slot] = seed;
         if (a.probe && (bo.ext || bo.sh)) {  // one queue entry per slot per launch: no race
             uint4 q = a.probe[slot];
             q.y += bo.ext ? 1u : 0u;
             q.z += bo.sh ? 1u : 0u;
             a.probe[slot] = q;
+        }
+        if (STREAM && !bo.ext) {
+            ended = true;
+            const uint32_t lf = a.left[slot];
+            if (lf) {
+                a.left[slot] = lf - 1u;
+                regen = true;
+            }
         }
     }
     uint32_t pos, spos;
@@ -1409,11 +1434,72 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(ShadeArgs a) {
         a.ray_out[2 * (size_t)pos + 1] = bo.e1;
         a.state_out[pos] = make_float4(bo.nb.x, bo.nb.y, bo.nb.z, bitsf(seed));
         a.slot_out[pos] = slot;
+        if (STREAM) a.aux_out[pos] = aux + 1u;  // next bounce, same sample
     }
-    if (bo.sh) {
+    if (bo.sh) {  // the shadow trace adds the colour to L[colour.w] when unoccluded
         a.shadow_ray[2 * (size_t)spos] = bo.s0;
         a.shadow_ray[2 * (size_t)spos + 1] = bo.s1;
-        a.shadow_color[spos] = make_float4(bo.col.x, bo.col.y, bo.col.z, bitsf(slot));
+        a.shadow_color[spos] = make_float4(bo.col.x, bo.col.y, bo.col.z, bitsf(li));
+    }
+    if constexpr (STREAM) {
+        uint32_t ppos, rpos;
+        __syncthreads();  // block_append2's LDS words: every wave has read the first call's before the second writes
+        block_append2<kShadeBlock>(ended, a.splat_count, ppos, regen, a.regen_count, rpos);
+        const uint32_t par = (aux >> 16) & 1u;
+        if (ended) a.splat_q[ppos] = slot | (par << 31);
+        if (regen) a.regen[rpos] = slot | ((par ^ 1u) << 31);
+    }
+}
+
+// Streaming wavefront, first samples: every slot's sample 0 (the reference seed x + y W), both L
+// parities cleared, spp - 1 samples left; queue entry i holds slot order[i] (cost order) or i.
+__global__ __launch_bounds__(kBlock) void k_stream_start(RaygenArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t sl = a.order ? a.order[i] : i;
+    const uint32_t px = a.pixel[sl];
+    const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
+    uint32_t seed = (uint32_t)(x + y * a.cam.width);
+    float4 r0, r1;
+    camera_ray(a.cam, x, y, seed, r0, r1);
+    a.L[sl] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a.L[sl + a.n] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a.left[sl] = a.spp - 1u;
+    a.ray_out[2 * (size_t)i] = r0;
+    a.ray_out[2 * (size_t)i + 1] = r1;
+    a.state_out[i] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
+    a.slot_out[i] = sl;
+    a.aux_out[i] = 0u;
+    if (a.probe) a.probe[sl].y += 1u;  // the camera ray (always traced)
+    if (i == 0) *a.count_out = a.n;
+}
+
+// Streaming wavefront, regeneration: each queued sample's camera ray from the slot's sampler state
+// (written by the shade that ended the slot's previous sample), appended behind the extension rays.
+__global__ __launch_bounds__(kBlock) void k_raygen_stream(RaygenArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = *a.regen_count;
+    if (blockIdx.x * kBlock >= n) return;  // uniform, before the barrier
+    const bool want = i < n;
+    uint32_t sl = 0, par = 0, seed = 0;
+    float4 r0 = {}, r1 = {};
+    if (want) {
+        const uint32_t e = a.regen[i];
+        sl = e & 0x7FFFFFFFu;
+        par = e >> 31;
+        const uint32_t px = a.pixel[sl];
+        seed = a.seed[sl];
+        camera_ray(a.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, r0, r1);
+        if (a.probe) a.probe[sl].y += 1u;
+    }
+    uint32_t pos, unused;
+    block_append2<kBlock>(want, a.count_out, pos, false, a.count_out, unused);
+    if (want) {
+        a.ray_out[2 * (size_t)pos] = r0;
+        a.ray_out[2 * (size_t)pos + 1] = r1;
+        a.state_out[pos] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
+        a.slot_out[pos] = sl;
+        a.aux_out[pos] = par << 16;
     }
 }
 
@@ -1507,6 +1593,22 @@ __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
     float4 f = a.film[sl];
     splat_one(f, a.L[sl], a.ray_clamp);
     a.film[sl] = f;
+}
+
+// Streaming wavefront: Tile::add_sample (core/film.h:66-70) for each finished sample of the
+// iteration, after its last shadow result; the sample's L buffer is cleared for the slot's sample
+// after next (the same parity).  A slot finishes at most one sample per iteration, and its samples
+// finish in order, so the film sums are the sequential loop's.
+__global__ __launch_bounds__(kBlock) void k_splat_stream(SplatArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *a.queue_count) return;
+    const uint32_t e = a.queue[i];
+    const uint32_t sl = e & 0x7FFFFFFFu;
+    const size_t li = sl + (size_t)(e >> 31) * a.n_slots;
+    float4 f = a.film[sl];
+    splat_one(f, a.L[li], a.ray_clamp);
+    a.film[sl] = f;
+    a.L[li] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 // ------------------------------------------------------------------------------ persistent path
@@ -3097,7 +3199,18 @@ void launch_raygen(const RaygenArgs &a, hipStream_t st) {
 }
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
-    hipLaunchKernelGGL(k_shade, dim3((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock)), dim3(kShadeBlock), 0, st, a);
+    const dim3 grid((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock));
+    if (a.aux_in) hipLaunchKernelGGL(k_shade_t<true>, grid, dim3(kShadeBlock), 0, st, a);
+    else hipLaunchKernelGGL(k_shade_t<false>, grid, dim3(kShadeBlock), 0, st, a);
+}
+void launch_stream_start(const RaygenArgs &a, hipStream_t st) {
+    if (a.n) hipLaunchKernelGGL(k_stream_start, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
+}
+void launch_raygen_stream(const RaygenArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items) hipLaunchKernelGGL(k_raygen_stream, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+}
+void launch_splat_stream(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items) hipLaunchKernelGGL(k_splat_stream, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
 }
 void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st) {
     hipLaunchKernelGGL(k_store_word, dim3(1), dim3(64), 0, st, src, dst);

@@ -221,7 +221,9 @@ const char *akr_hip_last_error(const akr_hip_ctx *ctx);
  * "path_tab", "path_mix", "path_min_wait", "path_grid_pct", "path_prio";
  * the cost order: "path_order", "path_order_min_spp", "path_order_share_pixels", "path_order_share_min_spp",
  * "path_order_shift", "path_order_pair", "path_order_classes", "path_order_cap", "path_order_sub",
- * "path_order_pilot_spp", "wave_order" (the wavefront's camera rays in cost order).
+ * "path_order_pilot_spp", "wave_order" (the wavefront's camera rays in cost order); wavefront variants
+ * (off by default, measured slower): "wave_dual" (two half-frame pipelines), "wave_stream"
+ * (one streaming ray queue with per-slot sample regeneration).
  * "verify" (default 1): in-band film check after every render.  Test only: "pixel_probe" (record
  * akr_pixel_probe per slot), "fault_test" (raise the hang guard's fault word once), "ray_steps",
  * "serial_shadow", "any_far_first", "la_early_exit". */
@@ -333,6 +335,7 @@ int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
 #define AKR_FORM_PATH 2
 #define AKR_FORM_PATH_DEFER 3
 #define AKR_FORM_PATH_SPEC 4
+#define AKR_FORM_WAVE_STREAM 5 /* the wavefront's kernels over one streaming ray queue (option wave_stream) */
 int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered);
 /* The inputs of the last persistent render's form choice: its pixels per resident
  * lane x 1000, and the cost-ordering pilot's camera rays and their summed traversal steps; -1 when the

@@ -799,3 +799,26 @@ def test_wavefront_dual_pipelines_bit_exact(hip_ctx_factory, order):
             for spp, depth in ((3, 5), (2, 0), (2, 1), (4, 2)):
                 _check_render(ctx, orc, spp, depth, tiles, W, H, probe=True)
                 assert ctx.render_form() == {"form": "wavefront", "ordered": bool(order)}
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_wavefront_stream_bit_exact(hip_ctx_factory, order):
+    """The streaming wavefront (option wave_stream, DESIGN.md §0: one ray queue of every active slot's
+    current ray, whatever its bounce; a finished sample's next sample regenerated into the next
+    launch; splats after the sample's last shadow result) renders the oracle's image bit for bit,
+    final sampler states and per-pixel ray counts included: Glossy / Mix, image textures and a 100K
+    soup, depths 0-5 (with clamp), ragged and overlapping tiles, 1-9 spp, with and without the
+    cost-ordered first camera rays."""
+    for sc, W, H in ((mixed_scene((48, 48)), 48, 48), (textured_scene((48, 48)), 48, 48),
+                     (small_soup(100_000, (96, 54)), 96, 54)):
+        with hip_ctx_factory(0) as ctx:
+            cs, orc = _setup(ctx, sc)
+            ctx.set_option("path", 0)
+            ctx.set_option("wave_stream", 1)
+            ctx.set_option("path_order_min_spp", 0 if order else 10 ** 6)
+            ctx.set_option("path_order_share_min_spp", 0 if order else 10 ** 6)
+            tiles = [(0, 0, W, H), (5, 3, W - 7, H - 9), (W // 2, 0, W, H // 3)]
+            for spp, depth in ((3, 5), (2, 0), (1, 1), (4, 2), (9, 5)):
+                _check_render(ctx, orc, spp, depth, tiles, W, H, probe=True)
+                assert ctx.render_form() == {"form": "wavefront_stream", "ordered": bool(order)}
+            _check_render(ctx, orc, 5, 5, tiles, W, H, clamp=0.4, probe=True)
