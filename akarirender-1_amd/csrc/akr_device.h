@@ -308,6 +308,10 @@ struct PathProfile {
     // time split of B and C (ticks, wave-uniform clocks summed per wave): load issue, the explicit
     // wait for the loads, the dependent work after them
     unsigned long long tv_issue, tv_wait, tv_comp, tl_issue, tl_wait, tl_comp;
+    // time split of A (k_path): the park, the finished rays' results (t_shade above), the sample end
+    // with the splat, pixel fetch and camera ray, and the unpark with the new rays' start
+    unsigned long long tp_park, tp_next, tp_begin;
+    unsigned long long tp_load;    // of t_shade: until the hit's shading record is loaded
 };
 
 // Persistent path kernel (k_path): the whole sample loop of every pixel of the tile list.

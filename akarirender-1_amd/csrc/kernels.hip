@@ -89,6 +89,14 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+__device__ __forceinline__ unsigned long long wave_max(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint32_t lane_prefix(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -1236,14 +1244,18 @@ __device__ __forceinline__ int select_light_index(const SceneDev &s, const Tab &
 
 template <class Tab>
 __device__ __forceinline__ void shade_hit_tab(const SceneDev &s, const Tab &tab, uint32_t gid, float u, float v, V3 wo,
-                                              V3 beta, uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
+                                              V3 beta, uint32_t &seed, int depth, int max_depth, bool last, Bounce &o,
+                                              unsigned long long *t_load = nullptr) {
     o.emit = o.ext = o.sh = false;
+    unsigned long long t0 = 0;  // counting builds (t_load): ticks until the shading record is in
+    if (t_load) t0 = wall_clock64();
     const ShadeTri tr = s.tri[gid];
     // the whole record in one round trip: without this the compiler loads the material id alone, tests
     // it, then loads the rest (two dependent trips; whole frame -0.6 %, profiles/r21_shade_trip_ab.log)
     asm volatile("" ::"v"(tr.a.x), "v"(tr.a.y), "v"(tr.a.z), "v"(tr.a.w), "v"(tr.b.x), "v"(tr.b.y), "v"(tr.b.z),
                  "v"(tr.b.w), "v"(tr.c.x), "v"(tr.c.y), "v"(tr.c.z), "v"(tr.c.w), "v"(tr.d.x), "v"(tr.d.y), "v"(tr.d.z),
                  "v"(tr.d.w), "v"(tr.e.x), "v"(tr.e.y), "v"(tr.e.z));
+    if (t_load) *t_load += wall_clock64() - t0;
     const int32_t mid = (int32_t)fbits(tr.a.w);
     if (mid < 0) return;  // a null material ends the path (undefined in the reference)
     const V3 v0{tr.a.x, tr.a.y, tr.a.z}, v1{tr.b.x, tr.b.y, tr.b.z}, v2{tr.c.x, tr.c.y, tr.c.z};
@@ -2057,6 +2069,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     r.bgid = kNoHit;
     r.cur = r.leaf = AKR_CHILD_EMPTY;
     unsigned long long p_outer = 0, p_procs = 0, p_tp = 0, p_tt = 0, p_tl = 0, p_lanes = 0, p_t0 = 0, p_t = 0, p_tsh = 0;
+    unsigned long long p_tpark = 0, p_tnext = 0, p_tbegin = 0, p_tload = 0;  // counting build: the split of A
     if (COUNT) p_t0 = wall_clock64();
 
     while (true) {
@@ -2081,7 +2094,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             bool fresh = false, next_any = false, sample_end = false, start = false;
             float4 ra = {}, rb = {};
             unsigned long long p_ts = 0;
-            if (COUNT) p_ts = wall_clock64();
+            unsigned long long tl_phase = 0;  // counting build: this phase's wait for the shading records
+            if (COUNT) {
+                p_ts = wall_clock64();
+                p_tpark += p_ts - p_t;
+            }
             if (!busy && !done && fin) {
                 fin = false;
                 const uint32_t hgid = r.bgid;
@@ -2108,7 +2125,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     bo.emit = false; bo.sh = false; bo.ext = hgid & 1; bo.e0 = make_float4(wo.x, wo.y, wo.z, 1.f); bo.e1 = bo.e0; bo.nb = wo;
 #elif !defined(AKR_PATH_CALL_SHADE)  // inlined (default): 3 % faster than the out-of-line call once every load is global
                     shade_hit_tab(pa.sc, tab, hgid, r.bu, r.bv, wo, beta, seed, depth,
-                              pa.max_depth, depth == nb - 1, bo);
+                              pa.max_depth, depth == nb - 1, bo, COUNT ? &tl_phase : nullptr);
 #else
                     shade_hit_call(pa.sc, hgid, r.bu, r.bv, wo, beta, seed, depth,
                                    pa.max_depth, depth == nb - 1, bo);
@@ -2156,7 +2173,12 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
 #endif
                 }
             }
-            if (COUNT) p_tsh += wall_clock64() - p_ts;
+            if (COUNT) {
+                const unsigned long long t = wall_clock64();
+                p_tsh += t - p_ts;
+                p_ts = t;
+                p_tload += wave_max(tl_phase);  // wave-uniform: the shading lanes share the wait
+            }
             if (sample_end) {  // Tile::add_sample (core/film.h:66-70), in sample order
                 splat_one(film, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
                 if (--left == 0) {
@@ -2189,6 +2211,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 fresh = true;
             }
             asm volatile("" ::: "memory");
+            if (COUNT) {
+                const unsigned long long t = wall_clock64();
+                p_tnext += t - p_ts;
+                p_ts = t;
+            }
             path_unpark(s_park, tid, r, ff, any);  // the busy lanes' traversal continues unchanged
             if (fresh) {
                 any = next_any;
@@ -2199,6 +2226,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
                 fin = !busy;
             }
+            if (COUNT) p_tbegin += wall_clock64() - p_ts;
         }
         if (COUNT) {
             const unsigned long long t = wall_clock64();
@@ -2222,7 +2250,15 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         }
         if (COUNT) p_tl += wall_clock64() - p_t;
     }
-    if (COUNT) path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
+    if (COUNT) {
+        path_count_flush(pa, c, p_outer, p_procs, p_tp, p_tt, p_tl, p_t0, p_lanes, p_tsh);
+        if (__lane_id() == 0 && pa.prof) {
+            atomicAdd(&pa.prof->tp_park, p_tpark);
+            atomicAdd(&pa.prof->tp_next, p_tnext);
+            atomicAdd(&pa.prof->tp_begin, p_tbegin);
+            atomicAdd(&pa.prof->tp_load, p_tload);
+        }
+    }
 }
 
 __device__ __forceinline__ void path_park(uint32_t (*s_park)[kTraceBlock], uint32_t tid, const PathRay &r) {

@@ -143,6 +143,12 @@ def time_split(pp, counts):
     cl = counts["per_mode"]["closest"]
     sh = counts["per_mode"]["shadow"]
     out = {"processing": f(pp["t_proc"]), "shading": f(pp["t_shade"]),
+           # k_path only (0 for the other forms): the processing phase's park, its sample end with the
+           # splat / pixel fetch / camera ray, and the unpark with the new rays' start
+           "processing_split": {"park": f(pp.get("tp_park", 0)), "results": f(pp["t_shade"]),
+                                "results_record_load": f(pp.get("tp_load", 0)),
+                                "sample_end_fetch_camera": f(pp.get("tp_next", 0)),
+                                "unpark_ray_start": f(pp.get("tp_begin", 0))},
            "traversal": {"total": f(pp["t_trav"]), "issue": f(pp["tv_issue"]), "wait": f(pp["tv_wait"]),
                          "work": f(pp["tv_comp"])},
            "leaf": {"total": f(pp["t_leaf"]), "issue": f(pp["tl_issue"]), "wait": f(pp["tl_wait"]), "work": f(pp["tl_comp"])},

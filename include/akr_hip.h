@@ -318,8 +318,9 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
  * processing phases, traversal-loop iterations, ticks processing / traversing / in leaves / in
  * total, the longest wave's ticks, lanes processed, ticks of processing spent on finished rays'
  * results (shading), k_path_spec's speculative samples started / dropped, and the time split of the
- * traversal and leaf phases: ticks issuing their loads, waiting for them, working after them
- * (DESIGN.md §3.4).  Not part of the reference interface. */
+ * traversal and leaf phases: ticks issuing their loads, waiting for them, working after them, then
+ * k_path's processing split: the park, the sample end with splat / pixel fetch / camera ray, and the
+ * unpark with the new rays' start, and the shading's wait for the hit's record (out[19..22]).  Not part of the reference interface. */
 int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
 /* The last akr_hip_render's lookahead lanes per pixel and sample passes launched (diagnostic). */
