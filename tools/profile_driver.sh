@@ -12,6 +12,9 @@
 #   rq2    128-B requests as FETCH_SIZE counts them (TCC_BUBBLE), DRAM-bound requests, L2 hits / misses
 #   ta     texture-address / texture-data unit busy cycles and their stalls on the L1 (TA_BUSY_avr per
 #          TA instance against GRBM_GUI_ACTIVE): is the vector memory pipe's address rate the limit?
+#   lds    LDS and scalar-memory instructions and their in-flight levels (latency = level / count), the
+#          waves' total and waiting cycles: what the non-VMEM waits are
+#   mix    instruction mix per wave (VALU / SALU / branch / LDS / VMEM / SMEM)
 #   tcp    L1 (TCP) stall cycles (pending misses, data path to TA, tag conflicts) and its accesses
 # tools/prof_summary.py <tag> turns gpurun_out/prof_<tag>/ into profiles/<tag>_{summary.md,traffic.json}.
 # Usage (GPU box, repo root): [PASSES="rq rq2"] tools/profile_driver.sh <tag> [bench args]
@@ -31,6 +34,8 @@ declare -A PMC=(
     [ea]="TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"
     [rq]="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
     [rq2]="TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum TCC_MISS_sum TCC_HIT_sum"
+    [lds]="SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD"
+    [mix]="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAVES"
     [ta]="TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE"
     [tcp]="TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TOTAL_ACCESSES_sum GRBM_GUI_ACTIVE"
 )
