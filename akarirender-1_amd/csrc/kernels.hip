@@ -272,8 +272,10 @@ __device__ __forceinline__ f2 pk_fma(f2 a, float b, float c) {  // v_pk_fma_f32:
 // dpos, two bits per slot.  Entered slots are ranked by position without moving any data: the first
 // becomes `cur`, each other one is written straight to its stack entry sp + (number of entered
 // slots at later positions), so the earliest is popped first.
-template <bool ANY>
-__device__ __forceinline__ void wide_order_push(uint32_t order_lo, uint32_t order_hi, uint32_t dpos, const float (&t)[4],
+// NOPOP (A/B build AKR_ONE_POP): when no slot is entered, return true instead of popping, so the
+// caller pops at one site for this case and for a postponed leaf
+template <bool ANY, bool NOPOP = false>
+__device__ __forceinline__ bool wide_order_push(uint32_t order_lo, uint32_t order_hi, uint32_t dpos, const float (&t)[4],
                                                 const bool (&hit)[4], const uint32_t (&ref)[4], uint32_t &cur, float lim,
                                                 lds_u64 *s_stack, glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid,
                                                 uint32_t gtid, int &sp) {
@@ -283,8 +285,9 @@ __device__ __forceinline__ void wide_order_push(uint32_t order_lo, uint32_t orde
 #pragma unroll
     for (int k = 0; k < 4; k++) pm |= hit[k] ? (1u << pos[k]) : 0u;
     if (pm == 0) {
+        if constexpr (NOPOP) return true;
         cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, sp, lim);
-        return;
+        return false;
     }
     const uint32_t rest = pm & (pm - 1u);  // entered slots after the first: pushed
     if (sp + 4 <= kStackLds) {
@@ -314,6 +317,7 @@ __device__ __forceinline__ void wide_order_push(uint32_t order_lo, uint32_t orde
 #pragma unroll
     for (int k = 0; k < 4; k++) c = ((first >> pos[k]) & 1u) ? ref[k] : c;
     cur = c;
+    return false;
 }
 
 template <bool TIGHT, bool ANY>
@@ -380,10 +384,11 @@ __device__ __forceinline__ WideNode wide_load(const float4 *wn, uint32_t cur) {
     return nd;
 }
 
-template <bool ANY>
+template <bool ANY, bool NOPOP = false>
 __device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t &cur, V3 o, uint32_t dpos, V3 invd,
                                                     float tmin, float tmaxp, float best, lds_u64 *s_stack, glb_u64 *ovf,
-                                                    uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp) {
+                                                    uint32_t ovf_threads, uint32_t tid, uint32_t gtid, int &sp,
+                                                    bool *need_pop = nullptr) {
     const float4 h = nd.h;
     const uint4 c = nd.c, qa = nd.qa, qb = nd.qb;
     uint32_t meta = __float_as_uint(h.w);
@@ -446,8 +451,9 @@ __device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t
     }
     const int tested = (c.x != AKR_CHILD_EMPTY) + (c.y != AKR_CHILD_EMPTY) + (c.z != AKR_CHILD_EMPTY) +
                        (c.w != AKR_CHILD_EMPTY);
-    wide_order_push<ANY>(qb.z, qb.w, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf, ovf_threads, tid, gtid,
-                         sp);
+    const bool np = wide_order_push<ANY, NOPOP>(qb.z, qb.w, dpos, t, hit, ref, cur, ANY ? tmaxp : best, s_stack, ovf,
+                                                ovf_threads, tid, gtid, sp);
+    if (NOPOP) *need_pop = np;
     return tested;
 }
 
@@ -681,9 +687,16 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                     c_sleaf += busy ? 1 : 0;
                 }
                 if (STEPS) steps += busy ? 1 : 0;
+                // lean visits pop at one site with the leaf postponement below (as path_traverse);
+                // the pilot (STEPS) keeps its step metric's old loop, on which the form rule is calibrated
+                constexpr bool kOnePop = TIGHT && !STEPS;
+                bool need_pop = false;
                 if (WIDE && busy && is_internal(cur)) {
                     int nt;
-                    if (TIGHT)  // every wide-loop ray of the tight kernel is lean (others: exact lane)
+                    if (kOnePop)
+                        nt = visit_wide_lean_node<ANY, true>(wide_load(wn, cur), cur, o, dpos, invd, tmin, tmaxp, best,
+                                                             s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, &need_pop);
+                    else if (TIGHT)  // every wide-loop ray of the tight kernel is lean (others: exact lane)
                         nt = visit_wide_lean<ANY>(wn, cur, o, dpos, invd, tmin, tmaxp, best, s_stack, stack_ovf,
                                                   a.ovf_threads, tid, gtid, sp);
                     else
@@ -708,10 +721,14 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                                                       stack_ovf, a.ovf_threads, tid, gtid, sp);
                     if (COUNT) deep = deep || sp > kStackLds;
                 }
-                if (busy && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
+                if (busy && !need_pop && leaf == AKR_CHILD_EMPTY && is_leaf(cur)) {
                     leaf = cur;  // postpone the leaf and keep descending
-                    cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? tmax : best);
+                    need_pop = true;
                 }
+                // (an any-hit ray culls at the float below tmax, as the visit's own pop did: an entry at
+                // tmax holds no hit below it)
+                if (need_pop)
+                    cur = stack_pop(s_stack, stack_ovf, a.ovf_threads, tid, gtid, sp, ANY ? (kOnePop ? tmaxp : tmax) : best);
                 // leave for the leaf phase once at most kWhileExit lanes are still searching for
                 // their first leaf (0: every lane holds a leaf or is done — classic while-while),
                 // but not while nobody holds a leaf yet and someone still searches: the leaf phase
@@ -1679,6 +1696,7 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
     if constexpr (PRIO) counted = !lowp || __ballot(busy && !lowp) == 0;
     while (true) {
         [[maybe_unused]] unsigned long long tc = 0;
+        bool need_pop = false;  // the visit entered no slot: pop below
         if constexpr (COUNT) {
             c.strav++;
             c.sleaf += busy ? 1 : 0;
@@ -1695,20 +1713,27 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
             c.tv_issue += tb - ta;
             c.tv_wait += tc - tb;
             if (vis) {
-                const int nt = visit_wide_lean_node<false>(nd, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack,
-                                                           ovf, ovf_threads, tid, gtid, r.sp);
+                const int nt = visit_wide_lean_node<false, true>(nd, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best,
+                                                                 s_stack, ovf, ovf_threads, tid, gtid, r.sp, &need_pop);
                 c.box[kind] += nt;
                 c.visit[kind]++;
                 c.deep_now = c.deep_now || r.sp > kStackLds;
             }
         } else if (busy && is_internal(r.cur)) {
-            visit_wide_lean<false>(wn, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf, ovf_threads, tid,
-                                   gtid, r.sp);
+            const WideNode nd = wide_load(wn, r.cur);
+            visit_wide_lean_node<false, true>(nd, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best, s_stack, ovf,
+                                              ovf_threads, tid, gtid, r.sp, &need_pop);
         }
-        if (busy && r.leaf == AKR_CHILD_EMPTY && is_leaf(r.cur)) {
+        // One pop site per iteration, for a visit that entered no slot and for a leaf to postpone (a
+        // popped leaf is postponed in the next iteration: every ray visits the same nodes and leaves
+        // in the same order).  Popping at two sites chained two LDS round trips into one iteration
+        // whenever the first pop returned a leaf: one site runs the whole frame 4.3 % and the 8-way
+        // share 6.5 % faster (profiles/r21_one_pop_ab.log).
+        if (busy && !need_pop && r.leaf == AKR_CHILD_EMPTY && is_leaf(r.cur)) {
             r.leaf = r.cur;  // postpone the leaf and keep descending
-            r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
+            need_pop = true;
         }
+        if (need_pop) r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
         const unsigned long long searching = __ballot(busy && counted && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
         if constexpr (COUNT) {
             const bool stop = (uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
