@@ -49,7 +49,7 @@ constexpr int kRefillMinAny = AKR_REFILL_MIN_ANY;  // the same for occlusion (an
 #define AKR_WHILE_EXIT_ANY AKR_WHILE_EXIT
 #endif
 #ifndef AKR_WHILE_EXIT
-#define AKR_WHILE_EXIT 16
+#define AKR_WHILE_EXIT 12  // 16 before the r21 one-pop loop; 8 / 12 / 16 / 24 re-swept on it: profiles/r21_while_exit_ab.log
 #endif
 constexpr uint64_t kMaxWideNodes = 1ull << 26;  // 64-B wide nodes addressed by a 32-bit byte offset (visit_wide_lean)
 constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
