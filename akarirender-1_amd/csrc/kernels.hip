@@ -2244,7 +2244,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 beta = V3{1.0f, 1.0f, 1.0f};
                 depth = 0;
                 // the pixel's coordinates from a register set at its fetch: no dependent load per sample
-                // (measured: whole frame -0.6 %, 8-way -0.5 %, profiles/r21_px_reg_ab.log; the reload
+                // (measured: whole frame -0.6 %, profiles/r21_px_reg_ab.log; the reload
                 // was cheaper before the r21 traversal changes freed registers)
                 const uint32_t px = pxr;
                 camera_ray(pa.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, ra, rb);
@@ -3025,7 +3025,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     }
                 }
                 if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
-                    const uint32_t px = pa.pixel[pix];
+                    const uint32_t px = pa.pixel[pix];  // reloaded: a register shuffled to the helpers measured slower (profiles/r21_px_reg_spec_ab.log)
                     Lr = V3{0.0f, 0.0f, 0.0f};
                     beta = V3{1.0f, 1.0f, 1.0f};
                     depth = 0;
