@@ -12,7 +12,13 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent.parent          # .../akarirender-1_amd
-LIB_PATH = Path(os.environ.get("AKR_HIP_LIB", PKG_DIR / "libakr_hip.so"))  # override: build variants
+PRODUCT_LIB = PKG_DIR / "libakr_hip.so"
+# Timing experiments only (tools/experiments/: a patch applied to a copy of csrc, built beside it): the
+# override is honoured for a library under tools/experiments/lib/, never for another path
+EXPERIMENT_LIB_DIR = PKG_DIR.parent / "tools" / "experiments" / "lib"
+LIB_PATH = Path(os.environ.get("AKR_HIP_LIB", PRODUCT_LIB))
+if LIB_PATH != PRODUCT_LIB and LIB_PATH.resolve().parent != EXPERIMENT_LIB_DIR.resolve():
+    raise ImportError(f"AKR_HIP_LIB={LIB_PATH}: only tools/experiments/lib/*.so may replace the product library")
 GEN_PATH = PKG_DIR / "libakr_scenegen.so"
 
 
@@ -101,7 +107,7 @@ BUILDER_SAH, BUILDER_LBVH, BUILDER_SBVH = 0, 1, 2
 COLLAPSE_SAH, COLLAPSE_BALANCED = 0, 1   # akr_build_params::wide_collapse
 MAT_DIFFUSE, MAT_GLOSSY, MAT_EMISSIVE, MAT_MIX = 0, 1, 2, 3
 PROBE_SEED, PROBE_RAYS = 1, 2
-FORM_NAMES = {-1: None, 0: "wavefront", 1: "wavefront+lookahead", 2: "k_path", 3: "k_path_defer", 4: "k_path_spec", 5: "wavefront_stream"}
+FORM_NAMES = {-1: None, 0: "wavefront", 2: "k_path", 3: "k_path_defer", 4: "k_path_spec"}
 
 # numpy views of the POD structs (for vectorised ray/hit buffers)
 RAY_DTYPE = np.dtype([("o", np.float32, 3), ("tmin", np.float32), ("d", np.float32, 3), ("tmax", np.float32)])
@@ -178,7 +184,7 @@ def load_library() -> C.CDLL:
         if not LIB_PATH.exists():
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
         lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
-        variant = "AKR_HIP_LIB" in os.environ  # an A/B build may predate newer exports
+        variant = LIB_PATH != PRODUCT_LIB  # an experiment build may predate newer exports
         for name, (res, args) in EXPORTS.items():
             if variant and not hasattr(lib, name):
                 continue
@@ -462,7 +468,7 @@ class HipContext:
                                            max_ms=arr[i].max_ms) for i in range(n.value)}
 
     def render_info(self) -> dict:
-        """Lookahead lanes per pixel and sample passes of the last render."""
+        """Lanes per pixel (always 1) and sample passes of the last render (1 for a persistent form)."""
         lanes, passes = C.c_int32(0), C.c_int32(0)
         self._check(self.lib.akr_hip_render_info(self.h, C.byref(lanes), C.byref(passes)))
         return {"lanes": lanes.value, "passes": passes.value}

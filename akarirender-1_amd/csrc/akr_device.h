@@ -162,6 +162,23 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
     uint32_t step_cap;             // COUNT builds with ray_steps: a ray stops after this many steps (0: none;
                                    // the cost-ordered fetch's pilot, whose hits nobody reads)
+    const uint32_t *perm;          // optional: fetch position -> queue entry (the wavefront's ray order,
+                                   // option wave_sort); results go to the entry's own index
+};
+
+// Reordering of a wavefront ray queue by a spatial key (option wave_sort): a counting
+// sort of the entries' indices by (Morton cell of the key point in the scene box, direction octant)
+struct SortArgs {
+    const float4 *rays;            // the queue's records (o | tmin, d | tmax)
+    const uint32_t *count;         // its length (device)
+    uint32_t *key;                 // per entry
+    uint32_t *hist;                // [nbins]: zero before k_sort_keys; k_sort_scan zeroes it again
+    uint32_t *cursor;              // [nbins]: each bin's next free sorted position
+    uint32_t *perm;                // out: sorted position -> entry
+    float lo[3], scale[3];         // cell = (p - lo) * scale, clamped to [0, 2^bits)
+    uint32_t bits;                 // Morton bits per axis
+    uint32_t nbins;                // 2^(3 bits + 3)
+    uint32_t end_point;            // key point: o + d * tmax (finite tmax) instead of o
 };
 
 struct ShadeArgs {
@@ -184,18 +201,6 @@ struct ShadeArgs {
     int32_t depth;
     int32_t max_depth;
     int32_t last;                  // no extension ray is traced after this bounce
-    // streaming wavefront (option wave_stream): queue entries of every bounce depth and
-    // both sample parities in one launch; a finished sample goes to the splat queue and, while the
-    // slot has samples left, its next sample to the regeneration queue
-    const uint32_t *aux_in;        // per entry: depth | sample parity << 16 (nullptr: classic k_shade)
-    uint32_t *aux_out;
-    uint32_t *left;                // per slot: samples not yet started
-    uint32_t *regen;               // slot | parity << 31 of each sample to start
-    uint32_t *regen_count;
-    uint32_t *splat_q;             // slot | parity << 31 of each finished sample
-    uint32_t *splat_count;
-    uint32_t n_slots;              // L holds two parities of n_slots entries each
-    int32_t nb;                    // traced bounces per sample
 };
 
 // One AO bounce (cpu/integrator.cpp:46-56) for every queued camera hit: appends the AO ray to
@@ -222,39 +227,6 @@ struct AoResolveArgs {
     float occlude;
 };
 
-// Lookahead lanes.  A lane of a pixel runs "the sample that starts o draws after
-// the pixel's committed sampler state" for one planned offset o; after the pass, the chain of lanes
-// whose offsets are real sample boundaries (0, then each accepted lane's end offset) is accepted.
-// The R pixels active in a pass each get look_lanes(R) lanes; slot j = lane * R + r for the r-th
-// active pixel.
-struct LookArgs {
-    const uint32_t *pixel;         // per pixel: x | y << 16
-    uint32_t n_pix, spp, budget, lane_cap;
-    uint32_t max_draws;            // a sample draws at most this many numbers (4 + 6 max_depth)
-    uint32_t nbins;                // sample-length histogram bins (length 4 + 2 b)
-    uint32_t width;
-    uint32_t *commit, *done;       // per pixel: sampler state at its first unfinished sample, samples done
-    uint8_t *hist;                 // per pixel: [kLookBins] u8 sample-length counts
-    const uint32_t *act;           // this pass: active pixels (indices), count *nact
-    const uint32_t *nact;
-    uint32_t *act_next, *nact_next;  // k_la_accept appends the pixels left for the next pass
-    uint32_t *off;                 // [lane * R + r]: planned offset (kNoOffset = no lane)
-    const uint32_t *seed;          // per slot: final sampler state (k_shade)
-    uint32_t *acc;                 // per active pixel: accepted lanes
-    uint32_t *chain;               // [t * R + r]: the t-th accepted lane
-};
-constexpr uint32_t kLookBins = 32;
-constexpr uint32_t kLookMaxLanes = 64;
-constexpr uint32_t kNoOffset = 0xFFFFFFFFu;
-
-// lanes per active pixel: min(cap, max(1, round(budget / R)))
-__host__ __device__ inline uint32_t look_lanes(uint32_t R, uint32_t budget, uint32_t cap) {
-    if (R == 0) return 0;
-    uint64_t l = ((uint64_t)budget + R / 2) / R;
-    if (l < 1) l = 1;
-    return (uint32_t)(l < cap ? l : cap);
-}
-
 struct RaygenArgs {
     CameraDev cam;
     const uint32_t *pixel;         // per slot: x | y << 16
@@ -269,15 +241,6 @@ struct RaygenArgs {
     uint4 *probe;                  // optional, per slot (akr_pixel_probe): .y counts the camera ray
     const uint32_t *order;         // optional: queue position -> slot (the cost order)
     uint32_t slot_base;            // without `order`: queue position i holds slot slot_base + i
-    uint32_t lookahead;            // nonzero: k_raygen_lanes over the planned lanes of `look`
-    LookArgs look;
-    // streaming wavefront: k_stream_start (every slot's first sample, `left` = spp - 1) and
-    // k_raygen_stream (the regeneration queue's samples appended to the ray queue)
-    uint32_t *left;
-    uint32_t *aux_out;
-    uint32_t spp;
-    const uint32_t *regen;
-    const uint32_t *regen_count;
 };
 
 struct SplatArgs {
@@ -285,13 +248,8 @@ struct SplatArgs {
     float4 *film;
     uint32_t n;
     float ray_clamp;
-    const uint32_t *order;         // optional: slot of entry i (a half's share of the cost order) ...
+    const uint32_t *order;         // optional: slot of entry i (the cost order) ...
     uint32_t slot_base;            // ... else slot_base + i
-    uint32_t lookahead;            // nonzero: per active pixel of `look`, its accepted lanes in chain order
-    LookArgs look;
-    const uint32_t *queue;         // streaming wavefront: finished samples (slot | parity << 31) ...
-    const uint32_t *queue_count;   // ... and their count; L holds two parities of n_slots entries
-    uint32_t n_slots;
 };
 
 // k_path counting build: per-wave phase profile (wall clock, 100 MHz), summed over waves
@@ -338,7 +296,6 @@ struct PathArgs {
     uint32_t *fault;               // mapped host word: set when a wave stops on the hang guard (k_path_defer)
     uint32_t fault_test;           // test only: k_path_defer raises `fault` once at the end of the launch
     uint32_t spec_depth;           // k_path_spec: levels of the speculation tree (samples beyond the head)
-    uint32_t spec_alt;             // k_path_spec: the tree's one-bounce branches too
     uint32_t probe_clock;          // diagnostic (counting build, option "pixel_probe" 2): the probe's flags
                                    // carry the pixel's completion time, (wall clock >> 4) << 8 | flags
 };

@@ -53,11 +53,7 @@ __device__ __forceinline__ V2 lerp3(V2 a, V2 b, V2 c, float u, float v) {
 // Scalar sin/cos in f64 rounded to f32 (the correctly rounded f32 value), see DESIGN.md §4;
 // akr_trig.h's bounded-range f64 kernels (identical to glibc's f64 results after rounding on every
 // f32 in [-2 pi, 2 pi], tests/test_host.py).
-#ifdef AKR_PROBE_F32TRIG  // timing probe only (not bit-exact): the f32 library functions
-__device__ __forceinline__ void fsincos(float x, float &s, float &c) { s = sinf(x); c = cosf(x); }
-#else
 __device__ __forceinline__ void fsincos(float x, float &s, float &c) { trig_sincosf(x, s, c); }
-#endif
 
 // LCGSampler::next1d (kernel/sampler.h:60-63)
 __device__ __forceinline__ float lcg_next(uint32_t &s) {

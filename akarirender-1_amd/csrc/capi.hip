@@ -197,6 +197,8 @@ struct akr_hip_ctx {
     DBuf<akr_bvh4_node> d_wnodes;
     DBuf<float4> d_wleaves;          // leaf blob (see TraceArgs::wide_leaves)
     uint32_t wide_root_dev = AKR_CHILD_EMPTY;
+    uint64_t bvh_dev_bytes = 0;       // the uploaded wide nodes + leaf blob
+    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // root box (wavefront ray keys)
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
@@ -228,19 +230,7 @@ struct akr_hip_ctx {
     DBuf<float4> d_L[2];  // per-sample radiance, alternating by sample pass (passes overlap)
     DBuf<float4> d_sray[2], d_scolor[2];  // shadow queues, alternating by bounce
     DBuf<uint32_t> d_ao_slot[2];          // AO queues traced closest-hit (finite occlude): slots
-    // lookahead lanes: per pixel committed sampler state, samples done, sample-length
-    // histogram; per slot planned offset; per pass parity active list + count, accepted lanes, chain
-    DBuf<uint32_t> d_commit, d_done, d_off, d_act[2], d_acc[2], d_chain[2], d_nact;
-    DBuf<uint8_t> d_hist;
-    uint32_t *h_remain = nullptr;         // mapped host memory, [2]: pixels left after the pass of that parity
-    uint32_t *d_remain_host = nullptr;    // its device address
-    hipEvent_t ev_acc[2] = {nullptr, nullptr}, ev_rem[2] = {nullptr, nullptr};
-    int lookahead = 1;                    // 1 = off (default), 0 = on when it adds lanes, >= 2: on, lane cap
-    int64_t slot_target = 2000000;        // lookahead budget: path slots per pass
-    uint64_t cur_slots = 0;               // path slots the buffers of the current render hold
-    bool cur_look = false;
-    bool la_early_exit = true;            // diagnostic: false runs all spp passes
-    int last_lanes = 1, last_passes = 0;
+    int last_passes = 0;
     int32_t last_form = AKR_FORM_NONE, last_ordered = 0;  // akr_hip_render_form
     // Shadow traces run on a second stream, so the shadow trace of bounce b overlaps the closest-hit
     // trace of bounce b+1 (independent work): each persistent launch's tail is filled by the other.
@@ -299,7 +289,6 @@ struct akr_hip_ctx {
     int path_spec_depth = 3;   // option "path_spec_depth": samples in flight beyond a pixel's head (1-3, the
                                // speculation tree's levels; the r19 main line measured 2, 4, 8, 15 alike, 1 slower,
                                // profiles/r19_spec_depth.log)
-    bool path_spec_alt = false;  // option "path_spec_alt": the tree's one-bounce branches too (measured slower)
     // the last render's form inputs (akr_hip_render_form_inputs): pixels per lane x 1000, the pilot's
     // rays and their summed steps
     int64_t last_ppl1000 = 0, last_pilot_rays = -1, last_pilot_steps = -1;
@@ -351,19 +340,13 @@ struct akr_hip_ctx {
     // option "wave_order": the wavefront's camera rays queued in the cost order (costliest first in
     // each shard of the closest-hit launch), by the same rule and floors as the persistent kernels
     bool wave_order = true;
-    // option "wave_dual": the wavefront as two half-frame pipelines, one per internal stream (A/B
-    // option)
-    bool wave_dual = false;
-    // option "wave_stream": the streaming wavefront: one ray queue holding every
-    // active slot's current ray whatever its bounce, a finished sample's slot regenerated into the
-    // next launch, so every closest-hit launch carries about one ray per active slot instead of
-    // the shrinking queue of one bounce of one sample pass
-    bool wave_stream = false;
-    DBuf<float4> d_Ls;                          // two sample parities of per-slot radiance
-    DBuf<uint32_t> d_aux[2], d_left, d_regq, d_splq[2];
-    hipEvent_t ev_sm[4] = {}, ev_ss[4] = {}, ev_poll[8] = {};
-    uint32_t *h_spoll = nullptr, *d_spoll_host = nullptr;  // mapped: queue counts polled by the host
-    int64_t last_stream_iters = 0;
+    // option "wave_sort": the wavefront's extension-ray queues traced in the order of a spatial key
+    // (DESIGN.md §3.3): the Morton cell of the ray origin in a 2^wave_sort grid per axis over the scene
+    // box, then the direction octant (0 = off, 1..5 bits per axis); option "wave_sort_shadow": the shadow
+    // queues too, keyed by their origin on the light (1) or by the shaded point they end at (2)
+    int wave_sort = 0;
+    int wave_sort_shadow = 0;
+    DBuf<uint32_t> d_skey[2], d_shist[2], d_scursor[2], d_sperm_ext, d_sperm_sh[2];
     DBuf<uint4> d_pprobe;  // the path pilot's per-slot probe
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -433,19 +416,10 @@ struct akr_hip_ctx {
         for (auto e : pool) (void)hipEventDestroy(e);
         if (side) (void)hipStreamSynchronize(side);
         if (main_st) (void)hipStreamSynchronize(main_st);
-        for (hipEvent_t e : {ev_fork, ev_join, ev_join_main, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1],
-                             ev_acc[0], ev_acc[1], ev_rem[0], ev_rem[1]})
+        for (hipEvent_t e : {ev_fork, ev_join, ev_join_main, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1]})
             if (e) (void)hipEventDestroy(e);
-        if (h_remain) (void)hipHostFree(h_remain);
         if (h_check) (void)hipHostFree(h_check);
         if (h_sum) (void)hipHostFree(h_sum);
-        if (h_spoll) (void)hipHostFree(h_spoll);
-        for (hipEvent_t e : ev_sm)
-            if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : ev_ss)
-            if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : ev_poll)
-            if (e) (void)hipEventDestroy(e);
         if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_gather) (void)hipEventDestroy(ev_gather);
@@ -673,14 +647,8 @@ struct akr_hip_ctx {
         HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPCHK(hipStreamCreateWithPriority(&main_st, hipStreamNonBlocking, greatest));
         HIPCHK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, least));
-        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_join_main, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1],
-                              &ev_acc[0], &ev_acc[1], &ev_rem[0], &ev_rem[1]})
+        for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_join_main, &ev_shade[0], &ev_shade[1], &ev_shadow[0], &ev_shadow[1], &ev_splat[0], &ev_splat[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        // mapped, coherent: k_store_word writes the remaining-pixel count straight into it (no DMA
-        // copy whose completion the host has to trust through an event)
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_remain), 2 * sizeof(uint32_t),
-                             hipHostMallocMapped | hipHostMallocCoherent));
-        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_remain_host), h_remain, 0));
         HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_fault), sizeof(uint32_t),
                              hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_fault_host), h_fault, 0));
@@ -893,10 +861,8 @@ struct akr_hip_ctx {
     // Pixels of the tile list (tiles in order, row-major inside a tile) into d_pixel, expanded on
     // the device from the clipped tiles (the host loop over every pixel and the pageable upload of
     // its list cost 1.7 ms per 1080p render); sizes the queues and the per-pass counter sets.
-    // Returns the pixel count.  look_ok: the render may use lookahead lanes (cur_look); the path
-    // buffers are sized for it.
-    uint64_t setup_pixels(const akr_rect *tiles, int32_t n_tiles, size_t n_count_words, hipStream_t st,
-                          bool look_ok = false) {
+    // Returns the pixel count.
+    uint64_t setup_pixels(const akr_rect *tiles, int32_t n_tiles, size_t n_count_words, hipStream_t st) {
         require_ready();
         if (!cam_set) throw std::runtime_error("camera not set (call akr_hip_set_camera)");
         if (n_tiles < 0 || (n_tiles > 0 && !tiles)) throw std::runtime_error("invalid tile list");
@@ -912,13 +878,9 @@ struct akr_hip_ctx {
             N += (uint64_t)(x1 - x0) * (uint64_t)(y1 - y0);
         }
         if (N >= (1ull << 31)) throw std::runtime_error("too many pixels in one render call");
-        // lookahead: R active pixels get look_lanes(R) lanes, R * lanes <= max(N, budget + N / 2)
-        cur_look = look_ok && lookahead != 1 && look_lanes((uint32_t)N, look_budget(), look_cap()) >= 2;
-        cur_slots = cur_look ? std::max<uint64_t>(N, (uint64_t)look_budget() + N / 2) : N;
-        if (cur_slots >= (1ull << 31)) throw std::runtime_error("lookahead slot budget too large");
         serialize(st);
-        ensure_capacity(cur_slots);  // before any upload: a reallocation drops contents
-        d_counts.reserve(4 * n_count_words);  // two pass parities (x two half-frame pipelines, option wave_dual)
+        ensure_capacity(N);  // before any upload: a reallocation drops contents
+        d_counts.reserve(2 * n_count_words);  // two pass parities
         n_pix_last = N;
         if (N == 0) return 0;
         ensure_side_stream();
@@ -1015,9 +977,6 @@ struct akr_hip_ctx {
         return rg;
     }
 
-    uint32_t look_budget() const { return (uint32_t)std::min<int64_t>(slot_target, 1ll << 30); }
-    uint32_t look_cap() const { return lookahead >= 2 ? (uint32_t)lookahead : kLookMaxLanes; }
-
     uint64_t render(const akr_pt_params &p, const akr_rect *tiles, int32_t n_tiles, hipStream_t st) {
         if (p.spp < 0 || p.max_depth < 0) throw std::runtime_error("spp and max_depth must be >= 0");
         if (p.max_depth > 1000) throw std::runtime_error("max_depth too large");
@@ -1026,88 +985,38 @@ struct akr_hip_ctx {
         // two sets, alternating by pass, since consecutive passes overlap
         const int D = p.max_depth + 2;
         const size_t n_count_words = 2 * (size_t)D * kWorkStride + 2 * (size_t)D * kTraceWords;
-        last_lanes = 1;
         last_passes = 0;
         last_form = AKR_FORM_NONE;
         last_ordered = 0;
-        // lookahead needs every sample length in the histogram's range: max_depth <= 10
-        const bool look_ok = p.spp >= 2 && 3u * (uint32_t)p.max_depth + 1u <= kLookBins;
         probe_ok = false;
         probe_n = 0;
-        const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st, look_ok);
+        const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st);
         if (N == 0) return 0;
         if (unchecked_render) {  // a fault raised by an earlier render_device that ran without "verify"
             unchecked_render = false;
             if (done_recorded) HIPCHK(hipEventSynchronize(ev_done));
             check_fault("the previous render_device call (run without verify; reported by the next render)");
         }
-        uint4 *probe_p = nullptr;  // option "pixel_probe" (not with lookahead lanes)
-        if (probe && !cur_look) {
+        hipStream_t ms = main_st;
+        uint4 *probe_p = nullptr;  // option "pixel_probe"
+        if (probe) {
             d_probe.reserve(N);
-            HIPCHK(hipMemsetAsync(d_probe.p, 0, N * sizeof(uint4), main_st));
+            HIPCHK(hipMemsetAsync(d_probe.p, 0, N * sizeof(uint4), ms));
             probe_p = d_probe.p;
             probe_n = N;
             probe_ok = true;
         }
-        // Lookahead: lanes of a pixel run the samples that start at planned draw
-        // offsets from its committed sampler state; k_la_accept keeps the chain of lanes that start
-        // at real sample boundaries.  Slot j = lane * R + r over the pass's R active pixels.
-        const bool la = cur_look;
-        const uint64_t S = cur_slots;
-        hipStream_t ms = main_st;
-        LookArgs lk{};
-        if (la) {
-            d_commit.reserve(N);
-            d_done.reserve(N);
-            d_hist.reserve(N * kLookBins);
-            d_off.reserve(S);
-            for (int k = 0; k < 2; k++) {
-                d_act[k].reserve(N);
-                d_acc[k].reserve(N);
-                d_chain[k].reserve(S);
-            }
-            d_nact.reserve(2 * kWorkStride);
-            lk.pixel = d_pixel.p;
-            lk.n_pix = (uint32_t)N;
-            lk.spp = (uint32_t)p.spp;
-            lk.budget = look_budget();
-            lk.lane_cap = look_cap();
-            lk.max_draws = 4u + 6u * (uint32_t)p.max_depth;
-            lk.nbins = 3u * (uint32_t)p.max_depth + 1u;
-            lk.width = (uint32_t)cam.width;
-            lk.commit = d_commit.p;
-            lk.done = d_done.p;
-            lk.hist = d_hist.p;
-            lk.off = d_off.p;
-            lk.seed = d_seed.p;
-            last_lanes = (int)look_lanes((uint32_t)N, lk.budget, lk.lane_cap);
-        }
-        // the lookahead arguments of the pass with parity q (its active list, acceptance record)
-        auto look = [&](int q) {
-            LookArgs x = lk;
-            x.act = d_act[q].p;
-            x.nact = d_nact.p + (size_t)q * kWorkStride;
-            x.act_next = d_act[q ^ 1].p;
-            x.nact_next = d_nact.p + (size_t)(q ^ 1) * kWorkStride;
-            x.acc = d_acc[q].p;
-            x.chain = d_chain[q].p;
-            return x;
-        };
-        if (la) {
-            timed("la_init", ms, [&] { launch_la_init(lk, d_act[0].p, d_nact.p, ms); });
-            timed("la_plan", ms, [&] { launch_la_plan(look(0), (uint32_t)N, ms); });
-        }
         const SceneDev sd = scene_dev();
         const bool tight = !(exact_cull || (p.flags & AKR_PT_EXACT_CULL));
-        // Persistent path kernel: every sample of every pixel in one launch.  It
-        // runs the lean wide traversal only; the reference cull, the BVH2 kernel, a wide view whose
-        // frames exceed the lean test's bounds and lookahead lanes keep the wavefront form.
+    // Persistent path kernel: every sample of every pixel in one launch.  It
+        // runs the lean wide traversal only; the reference cull, the BVH2 kernel and a wide view whose
+        // frames exceed the lean test's bounds keep the wavefront form.
         // auto: the persistent kernel for scenes whose shading is constant Diffuse / Emissive; Glossy,
         // Mix or image textures diverge inside the traversal waves, and the wavefront's separate shade
         // kernel measured faster there (textured hall 11.5 vs 16.0 ms per 4K spp)
         const bool use_path = path_kernel == 1 || (path_kernel == 2 && (int64_t)N <= path_auto_pixels &&
                                                    (simple_shading || path_auto_complex));
-        if (use_path && tight && wide && !la && trace_args(nullptr).lean) {
+        if (use_path && tight && wide && trace_args(nullptr).lean) {
             if (p.spp > 0) {
                 HIPCHK(hipMemsetAsync(d_counts.p, 0, kWorkWords * sizeof(uint32_t), ms));
                 PathArgs pa{};
@@ -1127,7 +1036,6 @@ struct akr_hip_ctx {
                 pa.fault_test = fault_test ? 1u : 0u;
                 pa.probe_clock = probe_clock ? 1u : 0u;
                 pa.spec_depth = (uint32_t)path_spec_depth;
-                pa.spec_alt = path_spec_alt ? 1u : 0u;
                 // the shading's material / light / CDF tables in LDS when they fit
                 const bool tab = path_tab && path_tab_fits(n_mats, n_lights);
                 // pixels per resident lane of k_path (the occupancy query's grid)
@@ -1156,7 +1064,7 @@ struct akr_hip_ctx {
                 const bool tris_ok = path_defer_min_tris == 0 || (int64_t)n_tris() >= path_defer_min_tris;
                 // the BVH's device bytes against the Infinity Cache share: a cache-resident
                 // tree takes k_path_defer at any size, a larger one k_path_spec up to path_tail_ppl10
-                const uint64_t bvh_bytes = (uint64_t)d_wnodes.n * sizeof(akr_bvh4_node) + (uint64_t)d_wleaves.n * sizeof(float4);
+                const uint64_t bvh_bytes = bvh_dev_bytes;
                 const bool cache_resident = path_spec != 1 && p.max_depth <= 8 && bvh_bytes <= (uint64_t)path_cache_mb << 20;
                 const bool size_tail = path_spec == 2 ? (path_spec_pixels > 0 ? (int64_t)N <= path_spec_pixels : size_ok)
                                                       : (path_defer_pixels > 0 ? (int64_t)N <= path_defer_pixels : size_ok);
@@ -1212,7 +1120,7 @@ struct akr_hip_ctx {
             join_streams(st);
             return N;
         }
-        if (p.spp > 0) last_form = la ? AKR_FORM_LOOKAHEAD : AKR_FORM_WAVEFRONT;
+        if (p.spp > 0) last_form = AKR_FORM_WAVEFRONT;
         const int nb = p.max_depth == 0 ? 1 : p.max_depth;  // the trace at depth == max_depth can
                                                              // add nothing: skipped
         int64_t g = 0;  // bounce index over all passes: shadow queues alternate by its parity
@@ -1221,7 +1129,7 @@ struct akr_hip_ctx {
             const int order_min_spp = (int64_t)N <= path_order_share_pixels
                                           ? std::min(path_order_share_min_spp, path_order_min_spp)
                                           : path_order_min_spp;
-            if (wave_order && path_order != 0 && !la && p.spp >= order_min_spp && N >= 2) {
+            if (wave_order && path_order != 0 && p.spp >= order_min_spp && N >= 2) {
                 if (!order_warm) {
                     pixel_order((uint32_t)std::min<uint64_t>(N, 64), ms);
                     order_warm = true;
@@ -1231,107 +1139,40 @@ struct akr_hip_ctx {
             }
             last_ordered = worder ? 1 : 0;
         }
-        if (wave_stream && !la && p.spp > 0) return render_stream(p, N, nb, tight, sd, probe_p, worder, st);
-        // Two half-frame pipelines (option "wave_dual"): the slots split into two halves
-        // (two contiguous ranges of the queue order), each running its whole bounce chain — raygen,
-        // then per bounce closest-hit trace, shade, shadow trace, and the splat — on its own stream
-        // (half 0 on the main stream, half 1 on the side stream), so one half's kernels fill the CUs
-        // while the other half's trace launch drains.  The halves share nothing but the slot-indexed
-        // arrays, whose slots they split; each pixel's samples stay in order on its stream.
-        if (wave_dual && !la && p.spp > 0 && N >= 2 * (uint64_t)kTraceBlock) {
-            const uint32_t half[2] = {(uint32_t)(N / 2), (uint32_t)(N - N / 2)}, base[2] = {0, (uint32_t)(N / 2)};
-            hipStream_t hs[2] = {ms, side};
-            HIPCHK(hipEventRecord(ev_shade[0], ms));  // the side stream starts after the pilot's order
-            HIPCHK(hipStreamWaitEvent(side, ev_shade[0], 0));
-            DBuf<uint2> *ovf[2] = {&d_ovf, &d_ovf_side};
-            for (int s = 0; s < p.spp; s++) {
-                const int ps = s & 1;
-                last_passes++;
-                float4 *L = d_L[ps].p;
-                for (int h = 0; h < 2; h++) {
-                    hipStream_t hst = hs[h];
-                    const size_t bs = base[h];
-                    uint32_t *cnt = d_counts.p + (size_t)(2 * h + ps) * n_count_words;
-                    auto qcount = [&](int b) { return cnt + (size_t)b * kWorkStride; };
-                    auto scount = [&](int b) { return cnt + (size_t)(D + b) * kWorkStride; };
-                    auto work = [&](int b, int k) { return cnt + 2 * (size_t)D * kWorkStride + (size_t)(2 * b + k) * kTraceWords; };
-                    HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), hst));
-                    RaygenArgs rg = raygen_args(half[h], L, qcount(0), s == 0);
-                    rg.ray_out = d_ray0.p + 2 * bs;
-                    rg.state_out = d_state0.p + bs;
-                    rg.slot_out = d_slot0.p + bs;
-                    rg.probe = probe_p;
-                    rg.order = worder ? worder + bs : nullptr;
-                    rg.slot_base = (uint32_t)bs;
-                    timed("raygen", hst, [&] { launch_raygen(rg, hst); });
-                    for (int b = 0; b < nb; b++) {
-                        const bool odd = b & 1;
-                        TraceArgs t = trace_args(work(b, 0));
-                        t.rays = (odd ? d_ray1.p : d_ray0.p) + 2 * bs;
-                        t.count = qcount(b);
-                        t.hits = d_hit.p + bs;
-                        t.stack_ovf = ovf[h]->p;
-                        timed("trace_closest", hst, [&] { trace_launch(TRACE_CLOSEST, tight, t, half[h], hst); });
-                        ShadeArgs sh{};
-                        sh.sc = sd;
-                        sh.ray_in = (odd ? d_ray1.p : d_ray0.p) + 2 * bs;
-                        sh.state_in = (odd ? d_state1.p : d_state0.p) + bs;
-                        sh.slot_in = (odd ? d_slot1.p : d_slot0.p) + bs;
-                        sh.hit_in = d_hit.p + bs;
-                        sh.count_in = qcount(b);
-                        sh.ray_out = (odd ? d_ray0.p : d_ray1.p) + 2 * bs;
-                        sh.state_out = (odd ? d_state0.p : d_state1.p) + bs;
-                        sh.slot_out = (odd ? d_slot0.p : d_slot1.p) + bs;
-                        sh.count_out = qcount(b + 1);
-                        sh.shadow_ray = d_sray[0].p + 2 * bs;
-                        sh.shadow_color = d_scolor[0].p + bs;
-                        sh.shadow_count = scount(b);
-                        sh.seed = d_seed.p;
-                        sh.L = L;
-                        sh.depth = b;
-                        sh.max_depth = p.max_depth;
-                        sh.last = b == nb - 1;
-                        sh.probe = probe_p;
-                        timed("shade", hst, [&] { launch_shade(sh, half[h], hst); });
-                        if (b < p.max_depth) {
-                            TraceArgs ts = trace_args(work(b, 1));
-                            ts.stack_ovf = ovf[h]->p;  // the half's own stream: after its closest-hit trace
-                            ts.rays = d_sray[0].p + 2 * bs;
-                            ts.count = scount(b);
-                            ts.shadow_color = d_scolor[0].p + bs;
-                            ts.L = L;
-                            timed("trace_shadow", hst, [&] { trace_launch(TRACE_SHADOW, tight, ts, half[h], hst); });
-                        }
-                    }
-                    SplatArgs sp{};
-                    sp.L = L;
-                    sp.film = d_film.p;
-                    sp.n = half[h];
-                    sp.order = worder ? worder + bs : nullptr;
-                    sp.slot_base = (uint32_t)bs;
-                    sp.ray_clamp = p.ray_clamp;
-                    timed("splat", hst, [&] { launch_splat(sp, half[h], hst); });
+        // ray reordering (option wave_sort): [0] the extension queues on the main stream, [1] the shadow
+        // queues on the side stream, each with its own keys, histogram and cursors
+        const int sbits = wave_sort > 0 ? wave_sort : 3;
+        const bool sort_ext = wave_sort > 0 && nb > 1, sort_sh = wave_sort_shadow > 0 && p.max_depth > 0;
+        SortArgs sa[2] = {};
+        if (sort_ext || sort_sh) {
+            const uint32_t nbins = 1u << (3 * sbits + 3);
+            for (int q = 0; q < 2; q++) {
+                if (q == 0 ? !sort_ext : !sort_sh) continue;
+                d_skey[q].reserve(N);
+                if (d_shist[q].n < nbins) {
+                    d_shist[q].reserve(nbins);
+                    HIPCHK(hipMemsetAsync(d_shist[q].p, 0, nbins * sizeof(uint32_t), ms));  // k_sort_scan re-zeroes it
+                }
+                d_scursor[q].reserve(nbins);
+                SortArgs &x = sa[q];
+                x.key = d_skey[q].p;
+                x.hist = d_shist[q].p;
+                x.cursor = d_scursor[q].p;
+                x.bits = (uint32_t)sbits;
+                x.nbins = nbins;
+                x.end_point = q == 1 && wave_sort_shadow == 2 ? 1u : 0u;
+                for (int k = 0; k < 3; k++) {
+                    x.lo[k] = scene_lo[k];
+                    const float ext = scene_hi[k] - scene_lo[k];
+                    x.scale[k] = ext > 0.0f ? (float)(1 << sbits) / ext : 0.0f;
                 }
             }
-            last_form = AKR_FORM_WAVEFRONT;
-            if (probe_p) {
-                HIPCHK(hipEventRecord(ev_splat[0], side));
-                HIPCHK(hipStreamWaitEvent(ms, ev_splat[0], 0));
-                launch_probe_seed(d_seed.p, (uint32_t)N, probe_p, ms);
-            }
-            join_streams(st);
-            return N;
+            if (sort_ext) d_sperm_ext.reserve(N);
+            if (sort_sh)
+                for (int k = 0; k < 2; k++) d_sperm_sh[k].reserve(N);
         }
         for (int s = 0; s < p.spp; s++) {
             const int ps = s & 1;
-            // lookahead: stop once the pass before last finished every pixel (the last pass then
-            // found nothing to do); the host stays two passes ahead of the device
-            // (h_remain words are reset to the sentinel before each store is issued: a stale zero
-            // left by an earlier render, or a store not yet visible, can never end the render early)
-            if (la && s >= 2 && la_early_exit) {
-                HIPCHK(hipEventSynchronize(ev_rem[ps]));
-                if (read_mapped(h_remain + ps) == 0) break;
-            }
             last_passes++;
             uint32_t *cnt = d_counts.p + (size_t)ps * n_count_words;
             auto qcount = [&](int b) { return cnt + (size_t)b * kWorkStride; };
@@ -1341,13 +1182,9 @@ struct akr_hip_ctx {
             // L[ps] and the counter set were last used by pass s - 2, whose splat ends its side-stream work
             if (s >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ps], 0));
             HIPCHK(hipMemsetAsync(cnt, 0, n_count_words * sizeof(uint32_t), ms));
-            RaygenArgs rg = raygen_args(la ? (uint32_t)S : (uint32_t)N, L, qcount(0), s == 0);
+            RaygenArgs rg = raygen_args((uint32_t)N, L, qcount(0), s == 0);
             rg.probe = probe_p;
             rg.order = worder;
-            if (la) {
-                rg.lookahead = 1;
-                rg.look = look(ps);
-            }
             timed("raygen", ms, [&] { launch_raygen(rg, ms); });
             for (int b = 0; b < nb; b++, g++) {
                 const bool odd = b & 1;
@@ -1356,7 +1193,8 @@ struct akr_hip_ctx {
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
-                timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, S, ms); });
+                t.perm = sort_ext && b > 0 ? d_sperm_ext.p : nullptr;  // the camera rays keep the tile / cost order
+                timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
                 // shade refills shadow queue g % 2: the shadow trace of bounce g - 2 must be done
                 if (g >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_shadow[sq], 0));
                 ShadeArgs sh{};
@@ -1379,11 +1217,27 @@ struct akr_hip_ctx {
                 sh.max_depth = p.max_depth;
                 sh.last = b == nb - 1;
                 sh.probe = probe_p;
-                timed("shade", ms, [&] { launch_shade(sh, (uint32_t)S, ms); });
+                timed("shade", ms, [&] { launch_shade(sh, (uint32_t)N, ms); });
                 HIPCHK(hipEventRecord(ev_shade[sq], ms));
                 HIPCHK(hipStreamWaitEvent(side, ev_shade[sq], 0));
+                if (sort_ext && b + 1 < nb) {  // the next bounce's queue, in key order
+                    SortArgs x = sa[0];
+                    x.rays = sh.ray_out;
+                    x.count = qcount(b + 1);
+                    x.perm = d_sperm_ext.p;
+                    timed("sort", ms, [&] { launch_sort(x, (uint32_t)N, ms); });
+                }
                 if (b < p.max_depth) {
+                    if (sort_sh) {
+                        SortArgs x = sa[1];
+                        x.rays = d_sray[sq].p;
+                        x.count = scount(b);
+                        x.perm = d_sperm_sh[sq].p;
+                        hipStream_t sst = serial_shadow ? ms : side;
+                        timed("sort_shadow", sst, [&] { launch_sort(x, (uint32_t)N, sst); });
+                    }
                     TraceArgs ts = trace_args(work(b, 1));
+                    ts.perm = sort_sh ? d_sperm_sh[sq].p : nullptr;
                     ts.stack_ovf = d_ovf_side.p;  // concurrent with a main-stream trace
                     ts.rays = d_sray[sq].p;
                     ts.count = scount(b);
@@ -1391,7 +1245,7 @@ struct akr_hip_ctx {
                     ts.L = L;
                     // option serial_shadow (measurement): on the main stream, so the launch is timed alone
                     hipStream_t sst = serial_shadow ? ms : side;
-                    timed("trace_shadow", sst, [&] { trace_launch(TRACE_SHADOW, tight, ts, S, sst); });
+                    timed("trace_shadow", sst, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, sst); });
                 }
                 if (serial_shadow) {
                     HIPCHK(hipEventRecord(ev_shadow[sq], ms));
@@ -1400,25 +1254,9 @@ struct akr_hip_ctx {
                     HIPCHK(hipEventRecord(ev_shadow[sq], side));
                 }
             }
-            SplatArgs sp{};
-            if (la) {
-                // every lane's final sampler state is written by the pass's last shade; the next
-                // pass's active list (parity ps ^ 1) was last read by the splat of pass s - 1
-                const int ns = ps ^ 1;
-                if (s >= 1) HIPCHK(hipStreamWaitEvent(ms, ev_splat[ns], 0));
-                HIPCHK(hipMemsetAsync(d_nact.p + (size_t)ns * kWorkStride, 0, sizeof(uint32_t), ms));
-                timed("la_accept", ms, [&] { launch_la_accept(look(ps), (uint32_t)N, ms); });
-                reinterpret_cast<volatile uint32_t *>(h_remain)[ps] = kMappedSentinel;
-                launch_store_word(d_nact.p + (size_t)ns * kWorkStride, d_remain_host + ps, ms);
-                HIPCHK(hipEventRecord(ev_rem[ps], ms));
-                HIPCHK(hipEventRecord(ev_acc[ps], ms));
-                HIPCHK(hipStreamWaitEvent(side, ev_acc[ps], 0));
-                timed("la_plan", ms, [&] { launch_la_plan(look(ns), (uint32_t)N, ms); });
-                sp.lookahead = 1;
-                sp.look = look(ps);
-            }
             // Tile::add_sample on the side stream, after the pass's last shadow trace: the next
             // pass (its own L and counters) proceeds on the main stream meanwhile
+            SplatArgs sp{};
             sp.L = L;
             sp.film = d_film.p;
             sp.n = (uint32_t)N;
@@ -1428,181 +1266,6 @@ struct akr_hip_ctx {
         }
         // the last shade of every pass ran on the main stream and left each slot's sampler state
         if (probe_p && p.spp > 0) launch_probe_seed(d_seed.p, (uint32_t)N, probe_p, ms);
-        join_streams(st);
-        return N;
-    }
-
-    // The streaming wavefront (option wave_stream).  Iteration i on the main stream: the closest-hit
-    // trace of the queue (every active slot's current ray: camera rays and extension rays of any
-    // bounce), k_shade over its hits (emission into the sample's L, the NEE shadow ray into shadow
-    // queue i % 2, the extension ray into the next queue; a path that ends queues its sample for
-    // the splat and, while the slot has samples left, the slot's next sample for regeneration), and
-    // k_raygen_stream (the regenerated samples' camera rays, behind the extension rays).  On the
-    // side stream: the shadow trace of queue i % 2 (adding to L when unoccluded) and the splat of
-    // the samples that ended in iteration i, whose last shadow result is then in.  A slot has one
-    // ray in flight, its samples start in order and each starts from the sampler state its
-    // predecessor ended with, so every sample, its L additions (emission, then the NEE results in
-    // bounce order) and the film sums are the sequential loop's (cpu/integrator.cpp:124-134).
-    // Per-iteration counters come from a ring of four blocks; a block, the shadow queue and the
-    // splat queue of iteration i are reused by iteration i + 4 / i + 2 only after the side stream is
-    // done with them (events).  The host polls the queue count every 16 iterations through mapped
-    // memory, staying at most 48 iterations ahead of the device, and stops when the queue is empty.
-    uint64_t render_stream(const akr_pt_params &p, uint64_t N, int nb, bool tight, const SceneDev &sd, uint4 *probe_p,
-                           const uint32_t *worder, hipStream_t st) {
-        hipStream_t ms = main_st;
-        const uint32_t n = (uint32_t)N;
-        d_Ls.reserve(2 * N);
-        for (int k = 0; k < 2; k++) {
-            d_aux[k].reserve(N);
-            d_splq[k].reserve(N);
-        }
-        d_left.reserve(N);
-        d_regq.reserve(N);
-        if (!ev_sm[0]) {
-            for (int k = 0; k < 4; k++) {
-                HIPCHK(hipEventCreateWithFlags(&ev_sm[k], hipEventDisableTiming));
-                HIPCHK(hipEventCreateWithFlags(&ev_ss[k], hipEventDisableTiming));
-            }
-            for (int k = 0; k < 8; k++) HIPCHK(hipEventCreateWithFlags(&ev_poll[k], hipEventDisableTiming));
-            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_spoll), 8 * sizeof(uint32_t),
-                                 hipHostMallocMapped | hipHostMallocCoherent));
-            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_spoll_host), h_spoll, 0));
-        }
-        // ring block k: [queue count out | shadow count | regen count | splat count | 2 x trace work]
-        const size_t bw = 4 * (size_t)kWorkStride + 2 * (size_t)kTraceWords;
-        if (d_counts.n < 4 * bw) throw std::runtime_error("internal: stream counter ring");
-        auto blk = [&](int64_t i) { return d_counts.p + (size_t)(i & 3) * bw; };
-        auto qcnt = [&](int64_t i) { return blk(i); };
-        auto scnt = [&](int64_t i) { return blk(i) + kWorkStride; };
-        auto rcnt = [&](int64_t i) { return blk(i) + 2 * (size_t)kWorkStride; };
-        auto pcnt = [&](int64_t i) { return blk(i) + 3 * (size_t)kWorkStride; };
-        auto work = [&](int64_t i, int k) { return blk(i) + 4 * (size_t)kWorkStride + (size_t)k * kTraceWords; };
-        HIPCHK(hipMemsetAsync(d_counts.p, 0, 4 * bw * sizeof(uint32_t), ms));
-        {
-            RaygenArgs rg = raygen_args(n, d_Ls.p, qcnt(-1), true);  // iteration -1's queue: the first samples
-            rg.order = worder;
-            rg.probe = probe_p;
-            rg.left = d_left.p;
-            rg.aux_out = d_aux[0].p;
-            rg.spp = (uint32_t)p.spp;
-            timed("raygen", ms, [&] { launch_stream_start(rg, ms); });
-        }
-#ifdef AKR_STREAM_DEBUG  // debug build: every stage synchronised and checked, so a fault names its kernel
-        auto dbg = [&](const char *stage, int64_t it) {
-            const hipError_t e1 = hipStreamSynchronize(ms), e2 = hipStreamSynchronize(side);
-            if (e1 != hipSuccess || e2 != hipSuccess)
-                throw std::runtime_error(std::string("stream debug: ") + stage + " at iteration " + std::to_string(it) +
-                                         ": " + hipGetErrorString(e1 != hipSuccess ? e1 : e2));
-        };
-#else
-        auto dbg = [](const char *, int64_t) {};
-#endif
-        dbg("start", -1);
-        const int64_t cap_iters = (int64_t)p.spp * nb + 1;  // the longest chain: spp samples of nb traced bounces
-        int64_t i = 0;
-        bool empty = false;
-        for (; i < cap_iters && !empty; i++) {
-            const int q = (int)(i & 1);
-            if (i >= 4) HIPCHK(hipStreamWaitEvent(ms, ev_ss[i & 3], 0));  // block i & 3 free (iteration i - 4)
-            HIPCHK(hipMemsetAsync(blk(i), 0, bw * sizeof(uint32_t), ms));
-            TraceArgs t = trace_args(work(i, 0));
-            t.rays = q ? d_ray1.p : d_ray0.p;
-            t.count = qcnt(i - 1);
-            t.hits = d_hit.p;
-            timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
-            dbg("trace_closest", i);
-            // shadow queue, splat queue and L parity of iteration i - 2 are done with on the side stream
-            if (i >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_ss[(i - 2) & 3], 0));
-            ShadeArgs sh{};
-            sh.sc = sd;
-            sh.ray_in = q ? d_ray1.p : d_ray0.p;
-            sh.state_in = q ? d_state1.p : d_state0.p;
-            sh.slot_in = q ? d_slot1.p : d_slot0.p;
-            sh.aux_in = d_aux[q].p;
-            sh.hit_in = d_hit.p;
-            sh.count_in = qcnt(i - 1);
-            sh.ray_out = q ? d_ray0.p : d_ray1.p;
-            sh.state_out = q ? d_state0.p : d_state1.p;
-            sh.slot_out = q ? d_slot0.p : d_slot1.p;
-            sh.aux_out = d_aux[q ^ 1].p;
-            sh.count_out = qcnt(i);
-            sh.shadow_ray = d_sray[q].p;
-            sh.shadow_color = d_scolor[q].p;
-            sh.shadow_count = scnt(i);
-            sh.seed = d_seed.p;
-            sh.L = d_Ls.p;
-            sh.max_depth = p.max_depth;
-            sh.nb = nb;
-            sh.n_slots = n;
-            sh.left = d_left.p;
-            sh.regen = d_regq.p;
-            sh.regen_count = rcnt(i);
-            sh.splat_q = d_splq[q].p;
-            sh.splat_count = pcnt(i);
-            sh.probe = probe_p;
-            timed("shade", ms, [&] { launch_shade(sh, n, ms); });
-            dbg("shade", i);
-            RaygenArgs rg = raygen_args(n, d_Ls.p, qcnt(i), false);
-            rg.ray_out = q ? d_ray0.p : d_ray1.p;
-            rg.state_out = q ? d_state0.p : d_state1.p;
-            rg.slot_out = q ? d_slot0.p : d_slot1.p;
-            rg.aux_out = d_aux[q ^ 1].p;
-            rg.regen = d_regq.p;
-            rg.regen_count = rcnt(i);
-            rg.probe = probe_p;
-            timed("raygen", ms, [&] { launch_raygen_stream(rg, n, ms); });
-            dbg("raygen", i);
-            const bool poll = (i & 15) == 15;
-            if (poll) {
-                reinterpret_cast<volatile uint32_t *>(h_spoll)[(i >> 4) & 7] = kMappedSentinel;
-                launch_store_word(qcnt(i), d_spoll_host + ((i >> 4) & 7), ms);
-            }
-            HIPCHK(hipEventRecord(ev_sm[i & 3], ms));
-            HIPCHK(hipStreamWaitEvent(side, ev_sm[i & 3], 0));
-            if (p.max_depth > 0) {
-                TraceArgs ts = trace_args(work(i, 1));
-                ts.stack_ovf = d_ovf_side.p;  // concurrent with the next iteration's main-stream trace
-                ts.rays = d_sray[q].p;
-                ts.count = scnt(i);
-                ts.shadow_color = d_scolor[q].p;
-                ts.L = d_Ls.p;
-                timed("trace_shadow", side, [&] { trace_launch(TRACE_SHADOW, tight, ts, N, side); });
-                dbg("trace_shadow", i);
-            }
-            SplatArgs sp{};
-            sp.L = d_Ls.p;
-            sp.film = d_film.p;
-            sp.n = n;
-            sp.ray_clamp = p.ray_clamp;
-            sp.queue = d_splq[q].p;
-            sp.queue_count = pcnt(i);
-            sp.n_slots = n;
-            timed("splat", side, [&] { launch_splat_stream(sp, n, side); });
-            dbg("splat", i);
-            HIPCHK(hipEventRecord(ev_ss[i & 3], side));
-            if (poll) {
-                HIPCHK(hipEventRecord(ev_poll[(i >> 4) & 7], ms));
-                // the poll two back (32 iterations earlier): wait for it, stop once its queue was empty
-                const int64_t k = (i >> 4) - 2;
-                if (k >= 0) {
-                    HIPCHK(hipEventSynchronize(ev_poll[k & 7]));
-                    const uint32_t c = read_mapped(h_spoll + (k & 7));
-                    if (c == kMappedSentinel) throw std::runtime_error("stream poll: the device never stored the count");
-                    if (c == 0) empty = true;
-                }
-            }
-        }
-        last_stream_iters = i;
-        last_passes = p.spp;
-        last_form = AKR_FORM_WAVE_STREAM;
-        if (!empty) {  // ran to the cap: the queue must be empty now (every chain is at most cap long)
-            HIPCHK(hipStreamSynchronize(ms));
-            reinterpret_cast<volatile uint32_t *>(h_spoll)[0] = kMappedSentinel;
-            launch_store_word(qcnt(i - 1), d_spoll_host, ms);
-            HIPCHK(hipStreamSynchronize(ms));
-            if (read_mapped(h_spoll) != 0) throw std::runtime_error("stream: rays left after the longest chain");
-        }
-        if (probe_p) launch_probe_seed(d_seed.p, n, probe_p, ms);  // every slot's final sampler state
         join_streams(st);
         return N;
     }
@@ -1760,10 +1423,6 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "shadow_grid_pct") {
             if (value < 1 || value > 100) throw std::runtime_error("shadow_grid_pct must be in [1, 100]");
             ctx->shadow_grid_pct = (int)value;
-        } else if (k == "lookahead") {
-            if (value < 0 || value > (int64_t)kLookMaxLanes)
-                throw std::runtime_error("lookahead must be in [0, 64] (0 = auto, 1 = off, n = on with at most n lanes)");
-            ctx->lookahead = (int)value;
         } else if (k == "path") {
             if (value < 0 || value > 2) throw std::runtime_error("path must be 0 (wavefront), 1 (path kernel) or 2 (auto)");
             ctx->path_kernel = (int)value;
@@ -1825,11 +1484,15 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_spec = (int)value;
         } else if (k == "wave_order") {
             ctx->wave_order = value != 0;
+        } else if (k == "wave_sort") {
+            if (value < 0 || value > 5) throw std::runtime_error("wave_sort must be in [0, 5] (Morton bits per axis, 0 = off)");
+            ctx->wave_sort = (int)value;
+        } else if (k == "wave_sort_shadow") {
+            if (value < 0 || value > 2) throw std::runtime_error("wave_sort_shadow must be 0, 1 (origin) or 2 (end point)");
+            ctx->wave_sort_shadow = (int)value;
         } else if (k == "path_order_pilot_spp") {
             if (value < 0 || value > 64) throw std::runtime_error("path_order_pilot_spp must be in [0, 64]");
             ctx->path_order_pilot_spp = (int)value;
-        } else if (k == "path_spec_alt") {
-            ctx->path_spec_alt = value != 0;
         } else if (k == "path_spec_depth") {
             if (value < 1 || value > 3) throw std::runtime_error("path_spec_depth must be in [1, 3]");
             ctx->path_spec_depth = (int)value;
@@ -1842,10 +1505,6 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "path_tail_ppl10") {
             if (value < 0) throw std::runtime_error("path_tail_ppl10 must be >= 0");
             ctx->path_tail_ppl10 = value;
-        } else if (k == "wave_dual") {
-            ctx->wave_dual = value != 0;
-        } else if (k == "wave_stream") {
-            ctx->wave_stream = value != 0;
         } else if (k == "leaf_align") {
             if (value != 1 && value != 2 && value != 4 && value != 8) throw std::runtime_error("leaf_align must be 1, 2, 4 or 8");
             ctx->leaf_align = (int)value;
@@ -1871,11 +1530,6 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->fault_test = value != 0;
         } else if (k == "verify") {
             ctx->verify = value != 0;
-        } else if (k == "la_early_exit") {
-            ctx->la_early_exit = value != 0;
-        } else if (k == "slot_target") {
-            if (value < 1) throw std::runtime_error("slot_target must be >= 1");
-            ctx->slot_target = value;
         } else if (k == "rays_per_lane") {
             if (value < 1 || value > 64) throw std::runtime_error("rays_per_lane must be in [1, 64]");
             ctx->rays_per_lane = (int)value;
@@ -2069,6 +1723,19 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         ctx->d_wleaves.reserve(1);
         ctx->d_wnodes.upload(wn.data(), wn.size(), ctx->stream);
         ctx->d_wleaves.upload(blob.get(), words + pad, ctx->stream);
+        // the uploaded tree's bytes (the DBufs' capacities only grow), for the form rule
+        ctx->bvh_dev_bytes = (uint64_t)wn.size() * sizeof(akr_bvh4_node) + (uint64_t)(words + pad) * sizeof(float4);
+        // the scene box (the virtual root's child 0: the real root's box) for the wavefront's ray keys
+        for (int k = 0; k < 3; k++) ctx->scene_lo[k] = ctx->scene_hi[k] = 0.0f;
+        if (!b.nodes.empty()) {
+            const akr_bvh_node &r = b.nodes[0];
+            const float lo[3] = {r.bxy0[0], r.bxy0[2], r.bz[0]}, hi[3] = {r.bxy0[1], r.bxy0[3], r.bz[1]};
+            for (int k = 0; k < 3; k++)
+                if (std::isfinite(lo[k]) && std::isfinite(hi[k]) && hi[k] >= lo[k]) {
+                    ctx->scene_lo[k] = lo[k];
+                    ctx->scene_hi[k] = hi[k];
+                }
+        }
         HIPCHK(hipStreamSynchronize(ctx->stream));  // before the host staging vectors go away
         ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -2531,7 +2198,7 @@ int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n) {
 
 int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes) {
     return guard(ctx, [&] {
-        if (lanes) *lanes = ctx->last_lanes;
+        if (lanes) *lanes = 1;  // one sample per pixel in flight (the lookahead lanes are gone)
         if (passes) *passes = ctx->last_passes;
     });
 }

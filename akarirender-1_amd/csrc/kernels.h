@@ -14,14 +14,9 @@ int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st);
-// streaming wavefront (option wave_stream): first samples, regenerated samples, finished-sample splats
-void launch_stream_start(const RaygenArgs &a, hipStream_t st);
-void launch_raygen_stream(const RaygenArgs &a, uint32_t max_items, hipStream_t st);
-void launch_splat_stream(const SplatArgs &a, uint32_t max_items, hipStream_t st);
+// wavefront ray order (option wave_sort): keys + histogram, scan, placement of the queue's entries
+void launch_sort(const SortArgs &a, uint32_t max_items, hipStream_t st);
 void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st);
-void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st);
-void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st);
-void launch_la_accept(const LookArgs &a, uint32_t max_active, hipStream_t st);
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_ao_resolve(const AoResolveArgs &a, uint32_t max_items, hipStream_t st);
 // persistent path kernel forms

@@ -3,9 +3,7 @@
 //   k_trace<MODE,...>  BVH2 traversal, one ray per lane, LDS-resident stack, persistent waves that
 //                      refill idle lanes from the queue (TBVHAccelerator::intersect / occlude,
 //                      bvh-accelerator.h:488-547)
-//   k_raygen           camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86);
-//                      k_la_plan / k_raygen_lanes / k_la_accept: lookahead lanes (several samples of a pixel in
-//                      flight from predicted sampler states, accepted when the prediction held)
+//   k_raygen           camera rays for every path slot (pathtracer.h:61-64, camera.h:67-86)
 //   k_shade            hit -> emission / BSDF sample / NEE light sample, wave-ballot compaction
 //                      of live paths and shadow rays (pathtracer.h:69-132, 137-162)
 //   k_splat            Tile::add_sample per pixel, in sample order (core/film.h:66-70)
@@ -148,26 +146,7 @@ __device__ __forceinline__ bool is_leaf(uint32_t c) { return (c & AKR_CHILD_LEAF
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 typedef __attribute__((address_space(1))) unsigned long long glb_u64;
 
-// An LDS stack entry.  A/B build AKR_STACK16: the ref in a u32 array and the entry distance's top
-// 16 bits (a positive float truncated: never above the exact distance, so a pop culls no entry the
-// exact value would keep, and only the order-free extra visits of a few near-ties are added) in a
-// u16 array behind it: 6 B per entry, so 15 entries and the park area fit 32 KB per workgroup.
-#ifdef AKR_STACK16
-typedef __attribute__((address_space(3))) uint32_t lds_u32s;
-typedef __attribute__((address_space(3))) unsigned short lds_u16s;
-constexpr int kStackLdsU64 = (kStackLds * kTraceBlock * 6 + 7) / 8;
-__device__ __forceinline__ unsigned long long lds_get(const lds_u64 *s, int e, uint32_t tid) {
-    const lds_u32s *r = (const lds_u32s *)s;
-    const lds_u16s *t = (const lds_u16s *)(r + kStackLds * kTraceBlock);
-    return (unsigned long long)r[e * kTraceBlock + tid] | ((unsigned long long)t[e * kTraceBlock + tid] << 48);
-}
-__device__ __forceinline__ void lds_put(lds_u64 *s, int e, uint32_t tid, unsigned long long v) {
-    lds_u32s *r = (lds_u32s *)s;
-    lds_u16s *t = (lds_u16s *)(r + kStackLds * kTraceBlock);
-    r[e * kTraceBlock + tid] = (uint32_t)v;
-    t[e * kTraceBlock + tid] = (unsigned short)(v >> 48);
-}
-#else
+// An LDS stack entry: 8 B, [entry][thread]
 constexpr int kStackLdsU64 = kStackLds * kTraceBlock;
 __device__ __forceinline__ unsigned long long lds_get(const lds_u64 *s, int e, uint32_t tid) {
     return s[e * kTraceBlock + tid];
@@ -175,25 +154,11 @@ __device__ __forceinline__ unsigned long long lds_get(const lds_u64 *s, int e, u
 __device__ __forceinline__ void lds_put(lds_u64 *s, int e, uint32_t tid, unsigned long long v) {
     s[e * kTraceBlock + tid] = v;
 }
-#endif
-
 
 // Pop the next stacked node whose stored entry distance is not beyond `lim` (the reference
 // re-tests a popped node's box against the current best, bvh-accelerator.h:500-503).
 __device__ __forceinline__ uint32_t stack_pop(const lds_u64 *s_stack, const glb_u64 *ovf, uint32_t ovf_threads,
                                               uint32_t tid, uint32_t gtid, int &sp, float lim) {
-#ifdef AKR_POP2  // A/B build: the top two LDS entries in one ds_read2st64 (one round trip for a culled top)
-    while (sp >= 2 && sp <= kStackLds) {
-        const unsigned long long e1 = lds_get(s_stack, sp - 1, tid);
-        const unsigned long long e2 = lds_get(s_stack, sp - 2, tid);
-        if (!(__uint_as_float((uint32_t)(e1 >> 32)) > lim)) {
-            sp -= 1;
-            return (uint32_t)e1;
-        }
-        sp -= 2;
-        if (!(__uint_as_float((uint32_t)(e2 >> 32)) > lim)) return (uint32_t)e2;
-    }
-#endif
     // while no lane of the wave is past the LDS part, an LDS-only loop: the overflow branch's
     // exec-mask split stays out of the common pop (with the uniform push below: whole frame -1.8 %,
     // profiles/r21_uniform_ovf_ab.log)
@@ -225,22 +190,6 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
     const float4 q1 = nodesf[4 * (size_t)cur + 1];
     const float4 q2 = nodesf[4 * (size_t)cur + 2];
     const uint4 q3 = nodesu[4 * (size_t)cur + 3];
-#ifdef AKR_PROBE_EXTRA_LOAD  // bottleneck probe only: one more 16-B load per node visit
-    {
-        const float4 qx = nodesf[4 * (size_t)cur + (cur & 3)];
-        asm volatile("" ::"v"(qx.x), "v"(qx.y), "v"(qx.z), "v"(qx.w));
-    }
-#endif
-#ifdef AKR_PROBE_EXTRA_VALU  // bottleneck probe only: ~AKR_PROBE_EXTRA_VALU dependent VALU ops per visit
-    {
-        float x = q0.x;
-        for (int k = 0; k < AKR_PROBE_EXTRA_VALU; k++) {
-            x = x * 1.0001f;
-            asm volatile("" : "+v"(x));
-        }
-        asm volatile("" ::"v"(x));
-    }
-#endif
     const float t0 = box_test<TIGHT, FAST>(q0.x, q0.y, q0.z, q0.w, q2.x, q2.y, o, invd, tmin, tmax);
     const float t1 = box_test<TIGHT, FAST>(q1.x, q1.y, q1.z, q1.w, q2.z, q2.w, o, invd, tmin, tmax);
     const float lim = ANY ? tmax : best;
@@ -271,10 +220,6 @@ __device__ __forceinline__ void visit_node(const float4 *nodesf, const uint4 *no
 __device__ __forceinline__ float ubyte(uint32_t w, int k) {  // v_cvt_f32_ubyte{k}
     return (float)((w >> (8 * k)) & 0xFFu);
 }
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 pk_fma(f2 a, float b, float c) {  // v_pk_fma_f32: fmaf per element
-    return __builtin_elementwise_fma(a, f2{b, b}, f2{c, c});
-}
 
 // Continue with the first entered slot of a wide node in the BVH2 depth-first order and push the
 // other entered slots behind it, each with its entry distance; pop when no slot is entered.
@@ -283,8 +228,8 @@ __device__ __forceinline__ f2 pk_fma(f2 a, float b, float c) {  // v_pk_fma_f32:
 // dpos, two bits per slot.  Entered slots are ranked by position without moving any data: the first
 // becomes `cur`, each other one is written straight to its stack entry sp + (number of entered
 // slots at later positions), so the earliest is popped first.
-// NOPOP (A/B build AKR_ONE_POP): when no slot is entered, return true instead of popping, so the
-// caller pops at one site for this case and for a postponed leaf
+// NOPOP: when no slot is entered, return true instead of popping, so the caller pops at one site
+// for this case and for a postponed leaf
 template <bool ANY, bool NOPOP = false>
 __device__ __forceinline__ bool wide_order_push(uint32_t order_lo, uint32_t order_hi, uint32_t dpos, const float (&t)[4],
                                                 const bool (&hit)[4], const uint32_t (&ref)[4], uint32_t &cur, float lim,
@@ -402,18 +347,7 @@ __device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t
                                                     bool *need_pop = nullptr) {
     const float4 h = nd.h;
     const uint4 c = nd.c, qa = nd.qa, qb = nd.qb;
-    uint32_t meta = __float_as_uint(h.w);
-#ifdef AKR_PROBE_EXTRA_VALU  // bottleneck probe only: ~AKR_PROBE_EXTRA_VALU dependent VALU ops per visit
-    {
-        float x = h.x;
-        for (int k = 0; k < AKR_PROBE_EXTRA_VALU; k++) {
-            x = x * 1.0001f;
-            asm volatile("" : "+v"(x));
-        }
-        meta |= __float_as_uint(x) & 0u;
-        asm volatile("" : "+v"(meta));
-    }
-#endif
+    const uint32_t meta = __float_as_uint(h.w);
     constexpr float kRel = 0x1p-21f;   // 8u
     constexpr float kAbs = 0x1p-120f;  // covers an underflowing sc
     const float scx = __uint_as_float((meta & 0xFFu) << 23) * invd.x;
@@ -433,28 +367,11 @@ __device__ __forceinline__ int visit_wide_lean_node(const WideNode &nd, uint32_t
     float t[4];
     bool hit[4];
     uint32_t ref[4] = {c.x, c.y, c.z, c.w};
-#ifdef AKR_PK_FMA  // A/B build: the slot bounds two slots at a time (v_pk_fma_f32, the same fma per element)
-    f2 pnx[2], pfx[2], pny[2], pfy[2], pnz[2], pfz[2];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        pnx[j] = pk_fma(f2{ubyte(qnx, 2 * j), ubyte(qnx, 2 * j + 1)}, scx, nox);
-        pfx[j] = pk_fma(f2{ubyte(qfx, 2 * j), ubyte(qfx, 2 * j + 1)}, scx, fox);
-        pny[j] = pk_fma(f2{ubyte(qny, 2 * j), ubyte(qny, 2 * j + 1)}, scy, noy);
-        pfy[j] = pk_fma(f2{ubyte(qfy, 2 * j), ubyte(qfy, 2 * j + 1)}, scy, foy);
-        pnz[j] = pk_fma(f2{ubyte(qnz, 2 * j), ubyte(qnz, 2 * j + 1)}, scz, noz);
-        pfz[j] = pk_fma(f2{ubyte(qfz, 2 * j), ubyte(qfz, 2 * j + 1)}, scz, foz);
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-#ifdef AKR_PK_FMA
-        const float nx = pnx[k >> 1][k & 1], fx = pfx[k >> 1][k & 1], ny = pny[k >> 1][k & 1], fy = pfy[k >> 1][k & 1],
-                    nz = pnz[k >> 1][k & 1], fz = pfz[k >> 1][k & 1];
-#else
         const float nx = __builtin_fmaf(ubyte(qnx, k), scx, nox), fx = __builtin_fmaf(ubyte(qfx, k), scx, fox);
         const float ny = __builtin_fmaf(ubyte(qny, k), scy, noy), fy = __builtin_fmaf(ubyte(qfy, k), scy, foy);
         const float nz = __builtin_fmaf(ubyte(qnz, k), scz, noz), fz = __builtin_fmaf(ubyte(qfz, k), scz, foz);
-#endif
         const float tk = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
         const float m1 = fminf(fminf(fx, fy), fminf(fz, lim));
         t[k] = tk;
@@ -662,9 +579,9 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                 if (!busy) {
                     const uint32_t my = first + lane_prefix(idle);
                     if (my < s_hi && base < s_hi - s_lo) {
-                        idx = my;
-                        ra = a.rays[2 * (size_t)my];
-                        rb = a.rays[2 * (size_t)my + 1];
+                        idx = a.perm ? a.perm[my] : my;  // the sorted order's entry (option wave_sort)
+                        ra = a.rays[2 * (size_t)idx];
+                        rb = a.rays[2 * (size_t)idx + 1];
                         fresh = true;
                     }
                 }
@@ -874,6 +791,105 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
     }
 }
 
+// ------------------------------------------------------------------------------ ray reordering
+// Option wave_sort: before a closest-hit or shadow trace of the wavefront, the
+// queue's entries are ordered by a key — the Morton code of the ray's key point in a 2^bits grid over
+// the scene box, then its direction octant — so the lanes of a wave, and the waves of one XCD (its
+// shard of the queue), walk the same subtrees.  A counting sort of indices: the trace reads entry
+// perm[j] at position j and writes its result at the entry's own index, so nothing downstream moves
+// and every result is the unsorted one (each ray's traversal is independent of its neighbours).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // bit i -> bit 3 i (v < 2^10)
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t sort_key(const SortArgs &a, float4 r0, float4 r1) {
+    float p[3] = {r0.x, r0.y, r0.z};
+    if (a.end_point && isfinite(r1.w)) {
+        p[0] = r0.x + r1.x * r1.w;
+        p[1] = r0.y + r1.y * r1.w;
+        p[2] = r0.z + r1.z * r1.w;
+    }
+    const int g = 1 << a.bits;
+    uint32_t c[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float f = (p[k] - a.lo[k]) * a.scale[k];
+        const int q = f >= 0.0f ? (f < (float)g ? (int)f : g - 1) : 0;  // NaN -> 0
+        c[k] = (uint32_t)q;
+    }
+    const uint32_t oct = (r1.x > 0.0f ? 1u : 0u) | (r1.y > 0.0f ? 2u : 0u) | (r1.z > 0.0f ? 4u : 0u);
+    return ((spread3(c[0]) | (spread3(c[1]) << 1) | (spread3(c[2]) << 2)) << 3) | oct;
+}
+
+// One atomic per distinct key of a wave (the queue is coherent after the first sorted bounce, so a
+// wave holds few keys): the lanes of each key add their count at once.  Returns the lane's position
+// among the lanes of its key plus the value the atomic returned.
+__device__ __forceinline__ uint32_t wave_bin_add(bool active, uint32_t key, uint32_t *ctr) {
+    uint32_t out = 0;
+    unsigned long long left = __ballot(active);
+    while (left) {
+        const int leader = __ffsll((long long)left) - 1;
+        const uint32_t lk = (uint32_t)__shfl((int)key, leader);
+        const unsigned long long m = __ballot(active && key == lk);
+        uint32_t base = 0;
+        if ((int)__lane_id() == leader) base = atomicAdd(ctr + lk, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (active && key == lk) out = base + lane_prefix(m);
+        left &= ~m;
+    }
+    return out;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_keys(SortArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = *a.count;
+    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup
+    const bool act = i < n;
+    uint32_t k = 0;
+    if (act) {
+        k = sort_key(a, a.rays[2 * (size_t)i], a.rays[2 * (size_t)i + 1]);
+        a.key[i] = k;
+    }
+    (void)wave_bin_add(act, k, a.hist);
+}
+
+// One workgroup: cursor = exclusive prefix of hist, hist = 0 for the next sort
+constexpr int kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void k_sort_scan(SortArgs a) {
+    __shared__ uint32_t s_sum[kScanBlock];
+    const uint32_t per = (a.nbins + kScanBlock - 1) / kScanBlock, b0 = threadIdx.x * per;
+    uint32_t tot = 0;
+    for (uint32_t b = b0; b < b0 + per && b < a.nbins; b++) tot += a.hist[b];
+    s_sum[threadIdx.x] = tot;
+    __syncthreads();
+    for (int off = 1; off < kScanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= (uint32_t)off ? s_sum[threadIdx.x - off] : 0u;
+        __syncthreads();
+        s_sum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_sum[threadIdx.x] - tot;
+    for (uint32_t b = b0; b < b0 + per && b < a.nbins; b++) {
+        const uint32_t h = a.hist[b];
+        a.cursor[b] = run;
+        a.hist[b] = 0u;
+        run += h;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_place(SortArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = *a.count;
+    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup
+    const bool act = i < n;
+    const uint32_t k = act ? a.key[i] : 0u;
+    const uint32_t pos = wave_bin_add(act, k, a.cursor);
+    if (act) a.perm[pos] = i;
+}
+
 // ------------------------------------------------------------------------------------ raygen
 __device__ __forceinline__ void apply_rows(const float *m, float x, float y, float z, float w, float *r, int rows) {
     for (int i = 0; i < rows; i++) {
@@ -946,221 +962,6 @@ __device__ __forceinline__ uint32_t lcg_advance(uint32_t s, uint32_t n) {
         n >>= 1;
     }
     return ra * s + rc;
-}
-
-// ------------------------------------------------------------------------------- lookahead
-// DESIGN.md §3.7.  A pixel's samples are sequential only through its sampler state: sample s + 1
-// starts where sample s stopped drawing (cpu/integrator.cpp:124-134), and a sample draws 4 + 6 k
-// (+2) numbers for k scattering events.  A lane runs the sample starting o draws after the pixel's
-// committed state for a planned offset o; the lanes whose offsets turn out to be real sample
-// boundaries are exactly the sequential samples, so accepting the chain 0 -> end(0) -> ... keeps
-// every result bit-identical to the sequential loop.
-
-// Per pixel: committed state x + y W (the reference seed), no samples, empty length histogram;
-// pass 0's active list is every pixel.
-__global__ __launch_bounds__(kBlock) void k_la_init(LookArgs a, uint32_t *act0, uint32_t *nact0) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n_pix) return;
-    const uint32_t px = a.pixel[i];
-    a.commit[i] = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * (int)a.width);
-    a.done[i] = 0;
-    uint4 *h = reinterpret_cast<uint4 *>(a.hist + (size_t)i * kLookBins);
-    h[0] = make_uint4(0, 0, 0, 0);
-    h[1] = make_uint4(0, 0, 0, 0);
-    act0[i] = i;
-    if (i == 0) *nact0 = a.n_pix;
-}
-
-// Plans the lanes of each active pixel.  From its sample-length histogram take the m most frequent
-// lengths c_1..c_m (total frequency q_m); the offsets are every sum of at most d of them (a chain of
-// t samples whose lengths are all among the m is then accepted in full), with (m, d) maximising the
-// expected accepted chain sum_{t=1..d} q_m^t under C(d + m, m) <= lanes and d < samples left.
-// Without history: lengths 4 (camera miss) and max_draws (full-length path), equally likely.
-__global__ __launch_bounds__(kBlock) void k_la_plan(LookArgs a) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t R = *a.nact;
-    if (r >= R) return;
-    const uint32_t L = look_lanes(R, a.budget, a.lane_cap);
-    const uint32_t pix = a.act[r];
-    const uint32_t rem = a.spp - a.done[pix];
-    constexpr int kTop = 6;
-    uint32_t c[kTop];
-    float p[kTop];
-    int mav = 0;
-    {
-        const uint4 *hp = reinterpret_cast<const uint4 *>(a.hist + (size_t)pix * kLookBins);
-        const uint4 h0 = hp[0], h1 = hp[1];
-        uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-        uint32_t total = 0;
-        for (int b = 0; b < (int)kLookBins; b++) total += (w[b >> 2] >> (8 * (b & 3))) & 0xFFu;
-        if (total == 0) {
-            c[0] = 4u;
-            p[0] = 1.0f;
-            mav = 1;
-            if (a.max_draws != 4u) {
-                c[1] = a.max_draws;
-                p[0] = p[1] = 0.5f;
-                mav = 2;
-            }
-        } else {
-            for (; mav < kTop; mav++) {
-                uint32_t best = 0, bb = 0;
-                for (int b = 0; b < (int)kLookBins; b++) {
-                    const uint32_t v = (w[b >> 2] >> (8 * (b & 3))) & 0xFFu;
-                    if (v > best) {
-                        best = v;
-                        bb = (uint32_t)b;
-                    }
-                }
-                if (best == 0) break;
-                w[bb >> 2] &= ~(0xFFu << (8 * (bb & 3)));
-                c[mav] = 4u + 2u * bb;
-                p[mav] = (float)best / (float)total;
-            }
-        }
-    }
-    int bm = 1, bd = 0;
-    float be = -1.0f, q = 0.0f;
-    for (int m = 1; m <= mav; m++) {
-        q += p[m - 1];
-        uint64_t need = 1;  // C(d + m, m) lanes for depth d
-        int d = 0;
-        while ((uint32_t)d + 1 < rem) {
-            const uint64_t nx = need * (uint64_t)(d + 1 + m) / (uint64_t)(d + 1);
-            if (nx > L) break;
-            need = nx;
-            d++;
-        }
-        float e = 0.0f, qt = 1.0f;
-        for (int t = 1; t <= d; t++) {
-            qt *= q;
-            e += qt;
-        }
-        if (e > be * 1.0001f) {
-            be = e;
-            bm = m;
-            bd = d;
-        }
-    }
-    // breadth-first over multisets (non-decreasing length index); a repeated sum is one lane
-    uint32_t o[kLookMaxLanes];
-    uint8_t last[kLookMaxLanes];
-    uint32_t n = 1, lb = 0, le = 1;
-    o[0] = 0;
-    last[0] = 0;
-    for (int t = 1; t <= bd && n < L; t++) {
-        for (uint32_t e = lb; e < le && n < L; e++)
-            for (int i = last[e]; i < bm && n < L; i++) {
-                const uint32_t v = o[e] + c[i];
-                bool dup = false;
-                for (uint32_t k = 0; k < n; k++) dup = dup || o[k] == v;
-                if (dup) continue;
-                o[n] = v;
-                last[n] = (uint8_t)i;
-                n++;
-            }
-        lb = le;
-        le = n;
-    }
-    for (uint32_t k = 0; k < L; k++) a.off[(size_t)k * R + r] = k < n ? o[k] : kNoOffset;
-}
-
-// Lookahead raygen: one thread per planned lane (slot j = lane * R + r); camera ray of the sample
-// that starts at the lane's offset.
-__global__ __launch_bounds__(kBlock) void k_raygen_lanes(RaygenArgs a) {
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t R = *a.look.nact;
-    const uint32_t n = R * look_lanes(R, a.look.budget, a.look.lane_cap);
-    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup: before the barrier
-    bool want = false;
-    float4 r0 = {}, r1 = {};
-    uint32_t seed = 0;
-    if (j < n) {
-        const uint32_t o = a.look.off[j];
-        if (o != kNoOffset) {
-            const uint32_t pix = a.look.act[j % R];
-            const uint32_t px = a.pixel[pix];
-            seed = lcg_advance(a.look.commit[pix], o);
-            camera_ray(a.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, r0, r1);
-            a.L[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            want = true;
-        }
-    }
-    uint32_t pos, unused;
-    block_append2(want, a.count_out, pos, false, a.count_out, unused);
-    if (want) {
-        a.ray_out[2 * (size_t)pos] = r0;
-        a.ray_out[2 * (size_t)pos + 1] = r1;
-        a.state_out[pos] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
-        a.slot_out[pos] = j;
-    }
-}
-
-// After the pass's last shade (every lane's final sampler state written), per active pixel: each
-// lane's sample length (steps from its start state to its final state), the histogram update, the
-// accepted chain, the new committed state and the next pass's active list.
-__global__ __launch_bounds__(kBlock) void k_la_accept(LookArgs a) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t R = *a.nact;
-    if (blockIdx.x * kBlock >= R) return;  // uniform per workgroup: before the barrier
-    bool left = false;
-    uint32_t pix = 0;
-    if (r < R) {
-        const uint32_t L = look_lanes(R, a.budget, a.lane_cap);
-        pix = a.act[r];
-        const uint32_t base = a.commit[pix];
-        uint4 *hp = reinterpret_cast<uint4 *>(a.hist + (size_t)pix * kLookBins);
-        const uint4 h0 = hp[0], h1 = hp[1];
-        uint32_t w[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-        uint32_t o[kLookMaxLanes], e[kLookMaxLanes];
-        uint32_t n = 0;
-        for (uint32_t k = 0; k < L; k++) {
-            const uint32_t ok = a.off[(size_t)k * R + r];
-            if (ok == kNoOffset) break;
-            const uint32_t f = a.seed[(size_t)k * R + r];
-            uint32_t s = lcg_advance(base, ok), len = kNoOffset;
-            for (uint32_t d = 1; d <= a.max_draws; d++) {
-                s = 1103515245u * s + 12345u;
-                if (s == f) {
-                    len = d;
-                    break;
-                }
-            }
-            o[n] = ok;
-            e[n] = len == kNoOffset ? kNoOffset : ok + len;
-            n++;
-            if (len != kNoOffset && len >= 4u && !(len & 1u) && (len - 4u) / 2u < a.nbins) {
-                const uint32_t b = (len - 4u) / 2u, sh = 8 * (b & 3);
-                if (((w[b >> 2] >> sh) & 0xFFu) == 0xFFu)  // saturated: halve every count
-                    for (int q = 0; q < 8; q++) w[q] = (w[q] >> 1) & 0x7F7F7F7Fu;
-                w[b >> 2] += 1u << sh;
-            }
-        }
-        hp[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        hp[1] = make_uint4(w[4], w[5], w[6], w[7]);
-        const uint32_t done = a.done[pix], rem = a.spp - done;
-        uint32_t cur = 0, acc = 1;
-        a.chain[r] = 0;
-        while (acc < rem && e[cur] != kNoOffset) {
-            uint32_t nx = kNoOffset;
-            for (uint32_t k = 1; k < n; k++)
-                if (o[k] == e[cur]) {
-                    nx = k;
-                    break;
-                }
-            if (nx == kNoOffset) break;
-            a.chain[(size_t)acc * R + r] = nx;
-            acc++;
-            cur = nx;
-        }
-        a.commit[pix] = a.seed[(size_t)cur * R + r];
-        a.done[pix] = done + acc;
-        a.acc[r] = acc;
-        left = done + acc < a.spp;
-    }
-    uint32_t pos, unused;
-    block_append2(left, a.nact_next, pos, false, a.nact_next, unused);
-    if (left) a.act_next[pos] = pix;
 }
 
 // ------------------------------------------------------------------------------------- shade
@@ -1394,59 +1195,34 @@ __device__ __forceinline__ void shade_hit(const SceneDev &s, uint32_t gid, float
     shade_hit_tab(s, global_tab(s), gid, u, v, wo, beta, seed, depth, max_depth, last, o);
 }
 
-// Out-of-line copy for the persistent path kernels (build option AKR_PATH_CALL_SHADE): a call keeps the
-// shading code's registers out of the traversal loop's allocation, at the price of saving the live
-// values around it in scratch.  With flat loads it was the only spill-free form; with global loads
-// the inlined form measured 3 % faster.
-__device__ __noinline__ void shade_hit_call(const SceneDev s, uint32_t gid, float u, float v, V3 wo, V3 beta,
-                                            uint32_t &seed, int depth, int max_depth, bool last, Bounce &o) {
-    shade_hit(s, gid, u, v, wo, beta, seed, depth, max_depth, last, o);
-}
-
 // One bounce for every queued hit (wavefront form)
 #ifndef AKR_SHADE_BLOCK
 #define AKR_SHADE_BLOCK 256
 #endif
 constexpr int kShadeBlock = AKR_SHADE_BLOCK;  // threads per shade workgroup (one queue atomic each)
-// STREAM (the streaming wavefront, option wave_stream): every entry carries its bounce depth and its
-// sample's parity (two L buffers per slot, so a finished sample can wait for its last shadow result
-// while the slot's next sample accumulates); a sample whose path ends is queued for the splat and,
-// while the slot has samples left, its next sample for k_raygen_stream.  Each slot has exactly one
-// entry in flight, so the per-slot reads and writes below never race.
-template <bool STREAM>
-__global__ __launch_bounds__(kShadeBlock) void k_shade_t(ShadeArgs a) {
+__global__ __launch_bounds__(kShadeBlock) void k_shade(ShadeArgs a) {
     const uint32_t i = blockIdx.x * kShadeBlock + threadIdx.x;
     const uint32_t n = *a.count_in;
     if (blockIdx.x * kShadeBlock >= n) return;  // whole workgroup past the queue (uniform: before any barrier)
     Bounce bo;
     bo.ext = bo.sh = false;
-    uint32_t slot = 0, seed = 0, aux = 0, li = 0;
-    bool ended = false, regen = false;
+    uint32_t slot = 0, seed = 0;
     if (i < n) {
         slot = a.slot_in[i];
-        li = slot;
-        int depth = a.depth;
-        bool last = a.last != 0;
-        if constexpr (STREAM) {
-            aux = a.aux_in[i];
-            depth = (int)(aux & 0xFFFFu);
-            last = depth == a.nb - 1;
-            li = slot + ((aux >> 16) & 1u) * a.n_slots;
-        }
         const float4 stv = a.state_in[i];
         seed = fbits(stv.w);
         const float4 hv = a.hit_in[i];
         const uint32_t gid = fbits(hv.w);
         if (gid != kNoHit) {  // miss -> on_miss (no-op), the path ends
             const float4 rdv = a.ray_in[2 * (size_t)i + 1];
-            shade_hit(a.sc, gid, hv.y, hv.z, neg(v3(rdv.x, rdv.y, rdv.z)), V3{stv.x, stv.y, stv.z}, seed, depth,
-                      a.max_depth, last, bo);
+            shade_hit(a.sc, gid, hv.y, hv.z, neg(v3(rdv.x, rdv.y, rdv.z)), V3{stv.x, stv.y, stv.z}, seed, a.depth,
+                      a.max_depth, a.last != 0, bo);
             if (bo.emit) {
-                float4 l = a.L[li];
+                float4 l = a.L[slot];
                 l.x += bo.e.x;
                 l.y += bo.e.y;
                 l.z += bo.e.z;
-                a.L[li] = l;
+                a.L[slot] = l;
             }
         }
         // the path does not reach another traced bounce: persist its sampler stream for the next
@@ -1458,14 +1234,6 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_t(ShadeArgs a) {
             q.z += bo.sh ? 1u : 0u;
             a.probe[slot] = q;
         }
-        if (STREAM && !bo.ext) {
-            ended = true;
-            const uint32_t lf = a.left[slot];
-            if (lf) {
-                a.left[slot] = lf - 1u;
-                regen = true;
-            }
-        }
     }
     uint32_t pos, spos;
     block_append2<kShadeBlock>(bo.ext, a.count_out, pos, bo.sh, a.shadow_count, spos);
@@ -1474,72 +1242,11 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_t(ShadeArgs a) {
         a.ray_out[2 * (size_t)pos + 1] = bo.e1;
         a.state_out[pos] = make_float4(bo.nb.x, bo.nb.y, bo.nb.z, bitsf(seed));
         a.slot_out[pos] = slot;
-        if (STREAM) a.aux_out[pos] = aux + 1u;  // next bounce, same sample
     }
     if (bo.sh) {  // the shadow trace adds the colour to L[colour.w] when unoccluded
         a.shadow_ray[2 * (size_t)spos] = bo.s0;
         a.shadow_ray[2 * (size_t)spos + 1] = bo.s1;
-        a.shadow_color[spos] = make_float4(bo.col.x, bo.col.y, bo.col.z, bitsf(li));
-    }
-    if constexpr (STREAM) {
-        uint32_t ppos, rpos;
-        __syncthreads();  // block_append2's LDS words: every wave has read the first call's before the second writes
-        block_append2<kShadeBlock>(ended, a.splat_count, ppos, regen, a.regen_count, rpos);
-        const uint32_t par = (aux >> 16) & 1u;
-        if (ended) a.splat_q[ppos] = slot | (par << 31);
-        if (regen) a.regen[rpos] = slot | ((par ^ 1u) << 31);
-    }
-}
-
-// Streaming wavefront, first samples: every slot's sample 0 (the reference seed x + y W), both L
-// parities cleared, spp - 1 samples left; queue entry i holds slot order[i] (cost order) or i.
-__global__ __launch_bounds__(kBlock) void k_stream_start(RaygenArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t sl = a.order ? a.order[i] : i;
-    const uint32_t px = a.pixel[sl];
-    const int x = (int)(px & 0xFFFFu), y = (int)(px >> 16);
-    uint32_t seed = (uint32_t)(x + y * a.cam.width);
-    float4 r0, r1;
-    camera_ray(a.cam, x, y, seed, r0, r1);
-    a.L[sl] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    a.L[sl + a.n] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    a.left[sl] = a.spp - 1u;
-    a.ray_out[2 * (size_t)i] = r0;
-    a.ray_out[2 * (size_t)i + 1] = r1;
-    a.state_out[i] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
-    a.slot_out[i] = sl;
-    a.aux_out[i] = 0u;
-    if (a.probe) a.probe[sl].y += 1u;  // the camera ray (always traced)
-    if (i == 0) *a.count_out = a.n;
-}
-
-// Streaming wavefront, regeneration: each queued sample's camera ray from the slot's sampler state
-// (written by the shade that ended the slot's previous sample), appended behind the extension rays.
-__global__ __launch_bounds__(kBlock) void k_raygen_stream(RaygenArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = *a.regen_count;
-    if (blockIdx.x * kBlock >= n) return;  // uniform, before the barrier
-    const bool want = i < n;
-    uint32_t sl = 0, par = 0, seed = 0;
-    float4 r0 = {}, r1 = {};
-    if (want) {
-        const uint32_t e = a.regen[i];
-        sl = e & 0x7FFFFFFFu;
-        par = e >> 31;
-        const uint32_t px = a.pixel[sl];
-        seed = a.seed[sl];
-        camera_ray(a.cam, (int)(px & 0xFFFFu), (int)(px >> 16), seed, r0, r1);
-        if (a.probe) a.probe[sl].y += 1u;
-    }
-    uint32_t pos, unused;
-    block_append2<kBlock>(want, a.count_out, pos, false, a.count_out, unused);
-    if (want) {
-        a.ray_out[2 * (size_t)pos] = r0;
-        a.ray_out[2 * (size_t)pos + 1] = r1;
-        a.state_out[pos] = make_float4(1.0f, 1.0f, 1.0f, bitsf(seed));
-        a.slot_out[pos] = sl;
-        a.aux_out[pos] = par << 16;
+        a.shadow_color[spos] = make_float4(bo.col.x, bo.col.y, bo.col.z, bitsf(slot));
     }
 }
 
@@ -1612,43 +1319,14 @@ __device__ __forceinline__ void splat_one(float4 &f, float4 l, float ray_clamp) 
     f.w += 1.0f;
 }
 
-// Tile::add_sample per pixel, in sample order (lookahead: each active pixel's accepted lanes in
-// chain order)
+// Tile::add_sample per pixel, in sample order
 __global__ __launch_bounds__(kBlock) void k_splat(SplatArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (a.lookahead) {
-        const uint32_t R = *a.look.nact;
-        if (i >= R) return;
-        const uint32_t pix = a.look.act[i], acc = a.look.acc[i];
-        float4 f = a.film[pix];
-        for (uint32_t t = 0; t < acc; t++) {
-            const uint32_t k = a.look.chain[(size_t)t * R + i];
-            splat_one(f, a.L[(size_t)k * R + i], a.ray_clamp);
-        }
-        a.film[pix] = f;
-        return;
-    }
     if (i >= a.n) return;
     const uint32_t sl = a.order ? a.order[i] : a.slot_base + i;
     float4 f = a.film[sl];
     splat_one(f, a.L[sl], a.ray_clamp);
     a.film[sl] = f;
-}
-
-// Streaming wavefront: Tile::add_sample (core/film.h:66-70) for each finished sample of the
-// iteration, after its last shadow result; the sample's L buffer is cleared for the slot's sample
-// after next (the same parity).  A slot finishes at most one sample per iteration, and its samples
-// finish in order, so the film sums are the sequential loop's.
-__global__ __launch_bounds__(kBlock) void k_splat_stream(SplatArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= *a.queue_count) return;
-    const uint32_t e = a.queue[i];
-    const uint32_t sl = e & 0x7FFFFFFFu;
-    const size_t li = sl + (size_t)(e >> 31) * a.n_slots;
-    float4 f = a.film[sl];
-    splat_one(f, a.L[li], a.ray_clamp);
-    a.film[sl] = f;
-    a.L[li] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 // ------------------------------------------------------------------------------ persistent path
@@ -1672,10 +1350,6 @@ __global__ __launch_bounds__(kBlock) void k_splat_stream(SplatArgs a) {
 #define AKR_PATH_WAVES 4
 #endif
 
-__device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
-    return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
-}
-
 // One lane's ray in the persistent path kernels' traversal loop (k_trace's registers) and the
 // counting build's tallies ([0] closest-hit rays, [1] shadow rays).
 struct PathRay {
@@ -1696,15 +1370,10 @@ struct PathCount {
 };
 
 // B. k_trace's traversal phase over every busy lane's ray (all rays here are lean)
-// PRIO (k_path_spec, A/B build AKR_SPEC_PRIO): lanes running a speculative sample (`lowp`) do not
-// hold the wave in the loop while a committed-path lane is busy: the early exit counts only the
-// others' searching lanes.
-template <bool COUNT, bool PRIO = false>
+template <bool COUNT>
 __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, const float4 *wn, lds_u64 *s_stack,
                                               glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
-                                              PathCount &c, bool lowp = false) {
-    bool counted = true;  // this lane's search counts for the early exit
-    if constexpr (PRIO) counted = !lowp || __ballot(busy && !lowp) == 0;
+                                              PathCount &c) {
     while (true) {
         [[maybe_unused]] unsigned long long tc = 0;
         bool need_pop = false;  // the visit entered no slot: pop below
@@ -1745,7 +1414,7 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
             need_pop = true;
         }
         if (need_pop) r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
-        const unsigned long long searching = __ballot(busy && counted && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
+        const unsigned long long searching = __ballot(busy && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
         if constexpr (COUNT) {
             const bool stop = (uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
                               (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0);
@@ -1855,27 +1524,9 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
 // others are traced inline with the exact BVH2 walk and come back finished (false).  An occlusion
 // ray's best starts at tmax (§3.8).  A return value, not bool references: a reference to one of two
 // flags picked per lane puts both in scratch.
-// The root node's box (the BVH2 root's, as path_begin tests it): A/B build AKR_ROOT_SGPR loads it once
-// per wave into wave-uniform registers instead of once per fresh ray
-struct RootBox {
-    float v[6];
-};
-__device__ __forceinline__ RootBox root_box(const TraceArgs &a) {
-    RootBox b{};
-#ifdef AKR_ROOT_SGPR
-    const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
-    const float4 r0 = nodesf[0], r2 = nodesf[2];
-    const float w[6] = {r0.x, r0.y, r0.z, r0.w, r2.x, r2.y};
-#pragma unroll
-    for (int k = 0; k < 6; k++) b.v[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(w[k])));
-#endif
-    return b;
-}
-
 template <bool COUNT>
 __device__ __forceinline__ bool path_begin(const TraceArgs &a, bool occl, float4 ra, float4 rb, PathRay &r,
-                                           lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid, PathCount &c,
-                                           const RootBox &rbx) {
+                                           lds_u64 *s_stack, glb_u64 *ovf, uint32_t tid, uint32_t gtid, PathCount &c) {
     r.o = V3{ra.x, ra.y, ra.z};
     r.d = V3{rb.x, rb.y, rb.z};
     r.tmin = ra.w;
@@ -1904,15 +1555,9 @@ __device__ __forceinline__ bool path_begin(const TraceArgs &a, bool occl, float4
         c.box[occl]++;
         c.deep_now = false;
     }
-#ifdef AKR_ROOT_SGPR
-    const float tr = box_test<true, true>(rbx.v[0], rbx.v[1], rbx.v[2], rbx.v[3], rbx.v[4], rbx.v[5], r.o, r.invd, r.tmin,
-                                          r.tmax);
-#else
-    (void)rbx;
     const float4 *nodesf = reinterpret_cast<const float4 *>(a.nodes);
     const float4 r0 = nodesf[0], r2 = nodesf[2];
     const float tr = box_test<true, true>(r0.x, r0.y, r0.z, r0.w, r2.x, r2.y, r.o, r.invd, r.tmin, r.tmax);
-#endif
     r.cur = (a.wide_root == AKR_CHILD_EMPTY || tr < 0.0f || tr > r.best) ? AKR_CHILD_EMPTY : a.wide_root;
     return true;
 }
@@ -2084,7 +1729,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;  // the trace at depth == max_depth is skipped (§3.3)
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
-    const RootBox rbx = root_box(a);
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -2157,15 +1801,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 } else {
                     const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
                     Bounce bo;
-#ifdef AKR_PROBE_NOSHADE  // timing probe only: no shading
-                    bo.emit = false; bo.sh = false; bo.ext = hgid & 1; bo.e0 = make_float4(wo.x, wo.y, wo.z, 1.f); bo.e1 = bo.e0; bo.nb = wo;
-#elif !defined(AKR_PATH_CALL_SHADE)  // inlined (default): 3 % faster than the out-of-line call once every load is global
+                    // inlined: 3 % faster than an out-of-line call once every load is global
                     shade_hit_tab(pa.sc, tab, hgid, r.bu, r.bv, wo, beta, seed, depth,
                               pa.max_depth, depth == nb - 1, bo, COUNT ? &tl_phase : nullptr);
-#else
-                    shade_hit_call(pa.sc, hgid, r.bu, r.bv, wo, beta, seed, depth,
-                                   pa.max_depth, depth == nb - 1, bo);
-#endif
                     if (bo.emit) {
                         Lr.x += bo.e.x;
                         Lr.y += bo.e.y;
@@ -2175,21 +1813,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         beta = bo.nb;
                         depth++;
                     }
-#ifdef AKR_PROBE_NOSHADOW  // timing probe only (not exact): shadow rays are not traced
-                    bo.sh = false;
-#endif
-#ifdef AKR_NEXT_SELECT  // A/B build: value selects instead of branches (0 VGPRs spilled, the Bounce in scratch)
-                    const bool bsh = bo.sh, bext = bo.ext;
-                    ra = sel4(bsh, bo.s0, bo.e0);
-                    rb = sel4(bsh, bo.s1, bo.e1);
-                    scol = bsh ? bo.col : scol;
-                    pe0 = sel4(bsh, bo.e0, pe0);
-                    pe1 = sel4(bsh, bo.e1, pe1);
-                    pend = bsh ? bext : pend;
-                    next_any = bsh;
-                    fresh = bsh || bext;
-                    sample_end = !(bsh || bext);
-#else
                     if (bo.sh) {  // the shadow ray first, the extension ray waits behind it
                         ra = bo.s0;
                         rb = bo.s1;
@@ -2206,7 +1829,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     } else {
                         sample_end = true;
                     }
-#endif
                 }
             }
             if (COUNT) {
@@ -2263,7 +1885,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     pc_closest += any ? 0u : 1u;
                     pc_shadow += any ? 1u : 0u;
                 }
-                busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
+                busy = path_begin<COUNT>(a, any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
                 fin = !busy;
             }
             if (COUNT) p_tbegin += wall_clock64() - p_ts;
@@ -2388,7 +2010,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const int nb = pa.max_depth == 0 ? 1 : pa.max_depth;
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
-    const RootBox rbx = root_box(a);
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -2479,13 +2100,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
                         const int depth = s.depth();
                         Bounce bo;
-#ifndef AKR_PATH_CALL_SHADE  // inlined (default): 3 % faster than the out-of-line call once every load is global
                         shade_hit_tab(pa.sc, tab, hgid, r.bu, r.bv, wo, beta, seed, depth,
                                   pa.max_depth, depth == nb - 1, bo);
-#else
-                        shade_hit_call(pa.sc, hgid, r.bu, r.bv, wo, beta, seed, depth,
-                                       pa.max_depth, depth == nb - 1, bo);
-#endif
                         if (bo.emit) {
                             Lr.x += bo.e.x;
                             Lr.y += bo.e.y;
@@ -2629,7 +2245,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             path_unpark(s_park, tid, r, ff, kind_now == RAY_OWN_SHADOW || kind_now == RAY_FOREIGN);
             if (fresh) {
                 if (COUNT) pc_closest += occl ? 0u : 1u;  // own extension / camera rays
-                busy = path_begin<COUNT>(a, occl, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
+                busy = path_begin<COUNT>(a, occl, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
                 fin = !busy;
             }
         }
@@ -2740,11 +2356,10 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const uint32_t g_full = 4u + 6u * (uint32_t)pa.max_depth;  // draws of a full-length sample
     const uint32_t g_one = 4u + 6u;                             // draws of a one-bounce sample
     const uint32_t lvl_cap = min(pa.spec_depth, 3u);            // tree levels used (option path_spec_depth)
-    const bool tree = pa.spec_alt != 0 && g_one != g_full;      // one-bounce branches too (option path_spec_alt)
+    // the chain of full-length guesses only: the tree's one-bounce branches measured slower
     const uint32_t spp = pa.spp;
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
-    const RootBox rbx = root_box(a);
     PathCount c;
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
@@ -2954,7 +2569,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
             {
                 const uint32_t left = spp - cseq;  // samples not committed
                 const bool avail = s.role() == ROLE_FREE && done;
-                const bool want = s.role() == ROLE_OWNER && s.nh() < (tree ? (2u << lvl_cap) - 2u : lvl_cap) && left > 1u;
+                const bool want = s.role() == ROLE_OWNER && s.nh() < lvl_cap && left > 1u;
                 const unsigned long long fm = __ballot(avail), owm = __ballot(want);
                 int nol = -1;  // a free lane's new owner
                 if (fm && owm) {
@@ -2998,7 +2613,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     const uint32_t lv_max = min(lvl_cap, spp - cseq - 1u);  // nodes past the last sample are useless
                     for (uint32_t k = 0; k < kSpecNodes && npick < nfree; k++) {
                         const uint32_t nd = (uint32_t)(kSpecNodeOrder >> (4u * k)) & 15u;
-                        if (((occ >> nd) & 1u) || node_lvl(nd) > lv_max || (node_code(nd) && !tree)) continue;
+                        if (((occ >> nd) & 1u) || node_lvl(nd) > lv_max || node_code(nd)) continue;
                         pick |= (unsigned long long)nd << (4u * npick);
                         npick++;
                         occ |= 1u << nd;
@@ -3045,7 +2660,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     sc_closest += next_any ? 0u : 1u;
                     sc_shadow += next_any ? 1u : 0u;
                 }
-                busy = path_begin<COUNT>(a, next_any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c, rbx);
+                busy = path_begin<COUNT>(a, next_any, ra, rb, r, s_stack, stack_ovf, tid, gtid, c);
                 fin = !busy;
             }
         }
@@ -3066,12 +2681,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         idle_rounds = 0;
         // ---- B. traversal phase, C. leaf phase (k_trace's, shared with the other persistent kernels)
         const int kd = s.any() ? 1 : 0;
-#ifdef AKR_SPEC_PRIO
-        path_traverse<COUNT, true>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c,
-                                   s.node() != 0u);
-#else
         path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
-#endif
         if (COUNT) {
             const unsigned long long t = wall_clock64();
             p_tt += t - p_t;
@@ -3266,42 +2876,23 @@ int trace_blocks_per_cu(int mode) {
 }
 
 void launch_raygen(const RaygenArgs &a, hipStream_t st) {
-    if (a.lookahead) {  // a.n: the slot capacity (the device decides how many are planned)
-        if (a.n) hipLaunchKernelGGL(k_raygen_lanes, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
-        return;
-    }
     if (a.n == 0) return;
     hipLaunchKernelGGL(k_raygen, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
 }
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     const dim3 grid((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock));
-    if (a.aux_in) hipLaunchKernelGGL(k_shade_t<true>, grid, dim3(kShadeBlock), 0, st, a);
-    else hipLaunchKernelGGL(k_shade_t<false>, grid, dim3(kShadeBlock), 0, st, a);
+    hipLaunchKernelGGL(k_shade, grid, dim3(kShadeBlock), 0, st, a);
 }
-void launch_stream_start(const RaygenArgs &a, hipStream_t st) {
-    if (a.n) hipLaunchKernelGGL(k_stream_start, dim3(blocks_for(a.n)), dim3(kBlock), 0, st, a);
-}
-void launch_raygen_stream(const RaygenArgs &a, uint32_t max_items, hipStream_t st) {
-    if (max_items) hipLaunchKernelGGL(k_raygen_stream, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
-}
-void launch_splat_stream(const SplatArgs &a, uint32_t max_items, hipStream_t st) {
-    if (max_items) hipLaunchKernelGGL(k_splat_stream, dim3(blocks_for(max_items)), dim3(kBlock), 0, st, a);
+void launch_sort(const SortArgs &a, uint32_t max_items, hipStream_t st) {
+    if (max_items == 0) return;
+    const dim3 grid(blocks_for(max_items));
+    hipLaunchKernelGGL(k_sort_keys, grid, dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanBlock), 0, st, a);
+    hipLaunchKernelGGL(k_sort_place, grid, dim3(kBlock), 0, st, a);
 }
 void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st) {
     hipLaunchKernelGGL(k_store_word, dim3(1), dim3(64), 0, st, src, dst);
-}
-void launch_la_init(const LookArgs &a, uint32_t *act0, uint32_t *nact0, hipStream_t st) {
-    if (a.n_pix == 0) return;
-    hipLaunchKernelGGL(k_la_init, dim3(blocks_for(a.n_pix)), dim3(kBlock), 0, st, a, act0, nact0);
-}
-void launch_la_plan(const LookArgs &a, uint32_t max_active, hipStream_t st) {
-    if (max_active == 0) return;
-    hipLaunchKernelGGL(k_la_plan, dim3(blocks_for(max_active)), dim3(kBlock), 0, st, a);
-}
-void launch_la_accept(const LookArgs &a, uint32_t max_active, hipStream_t st) {
-    if (max_active == 0) return;
-    hipLaunchKernelGGL(k_la_accept, dim3(blocks_for(max_active)), dim3(kBlock), 0, st, a);
 }
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;

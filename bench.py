@@ -347,11 +347,10 @@ def launch_check(world: int, rank: int):
         dist.destroy_process_group()
 
 
-# Untimed same-run legs of the other BASELINE configs (VERDICT r4 item 5): C2, the reference's Cornell
-# box at 1920x1080, and the C4 stand-in (the synthetic textured hall at 3840x2160).  Each renders a
-# bounded number of spp in the library's form for that scene; the metric's spp (1024 / 256) would add
-# ~2 s each, so they report Msamples/s at a smaller spp and say so.
-SIDE_LEGS = {"cornell": (1920, 1080, 64), "hall": (3840, 2160, 16)}
+# Untimed same-run legs of the other BASELINE configs (VERDICT r5 item 2): C2, the reference's Cornell
+# box at 1920x1080 and 1024 spp, and the C4 stand-in (the synthetic textured hall) at 3840x2160 and
+# 256 spp, each at its BASELINE spp in the library's form for that scene (~1.3 s and ~2.7 s).
+SIDE_LEGS = {"cornell": (1920, 1080, 1024), "hall": (3840, 2160, 256)}
 
 
 def side_leg(name, device, max_depth, tile, build_kw, stream_of):
@@ -433,15 +432,12 @@ def main():
     ap.add_argument("--timed-stats", type=int, default=-1,
                     help="HIP events inside the timed region: 2 = the dominant kernel (trace_closest) only, "
                          "1 = every kernel, 0 = none (probe), -1 = 1 on a whole frame, 2 on a share of a split")
-    ap.add_argument("--lookahead", type=int, default=1,
-                    help="speculative sample lanes per pixel (1 = off, 0 = on from --slot-target, n = at most n lanes)")
-    ap.add_argument("--slot-target", type=int, default=0, help="auto lookahead: path slots per render (0: library default)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
     ap.add_argument("--wavefront-spp", type=int, default=16,
                     help="untimed same-run leg in the wavefront form (north_star's layout), spp; 0 = skip")
     ap.add_argument("--side-legs", type=int, default=1,
-                    help="N = 1, soup: also render C2 (Cornell 1080p, 64 spp) and the C4 stand-in (hall 4K, 16 spp) "
+                    help="N = 1, soup: also render C2 (Cornell 1080p, 1024 spp) and the C4 stand-in (hall 4K, 256 spp) "
                          "as untimed legs of the same run (the line's `configs` block); 0 = skip")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearse the N-rank path on a one-GPU box: every rank on device 0, a gloo process group, "
@@ -526,9 +522,6 @@ def main():
     ctx.set_option("path", args.path)
     if not args.lean:
         ctx.set_option("lean", 0)
-    ctx.set_option("lookahead", args.lookahead)
-    if args.slot_target:
-        ctx.set_option("slot_target", args.slot_target)
     if args.shadow_grid_pct != 100:
         ctx.set_option("shadow_grid_pct", args.shadow_grid_pct)
     for kv in args.opt:
@@ -609,7 +602,7 @@ def main():
                            "mean_radiance": float(rrad.mean() / max(1, spp)), "adopted_bvh": adopted,
                            "reference": "one whole-frame akr_hip_render of rank 0's context"}
     kstats = ctx.kernel_stats()
-    la = ctx.render_info()
+    passes = ctx.render_info()["passes"]
     # sanity: every pixel of this rank got every sample of the timed render
     assert int(wgt[:npix].min().item()) == spp and int(wgt[:npix].max().item()) == spp
     # untimed per-kernel breakdown (events on every launch) over a few more samples
@@ -632,13 +625,12 @@ def main():
     # -> splat launches per bounce), when the timed render ran a persistent kernel
     wavefront = None
     if rank == 0 and args.wavefront_spp > 0 and form["form"] in ("k_path", "k_path_defer", "k_path_spec"):
-        # the plain wavefront (no lookahead lanes), whatever options the timed render ran with;
-        # the options in effect before are restored afterwards
-        saved = {k: ctx.option_set(k) for k in ("stats", "path", "lookahead")}
+        # the wavefront, whatever form the timed render ran; the options in effect before are
+        # restored afterwards
+        saved = {k: ctx.option_set(k) for k in ("stats", "path")}
         ctx.reset_stats()
         ctx.set_option("stats", 0)
         ctx.set_option("path", 0)
-        ctx.set_option("lookahead", 1)
         ctx.render_device(1, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)   # warm
         torch.cuda.synchronize(dev)
         tw = time.perf_counter()
@@ -661,7 +653,7 @@ def main():
     if split != world:  # scaling probe: one rank's share of an N-way split, on this GPU
         print(json.dumps({"probe": "emulated rank 0 of a tile split", "emulate_world": split, "rank_pixels": npix,
                           "spp": spp, "rank_ms_per_spp": round(elapsed / spp * 1e3, 4),
-                          "rank_Msamples_per_s": round(npix * spp / elapsed / 1e6, 3), "lookahead": la,
+                          "rank_Msamples_per_s": round(npix * spp / elapsed / 1e6, 3), "passes": passes,
                           "projected_node_Msamples_per_s": round(W * H * spp / elapsed / 1e6, 3),
                           "form": form, "wavefront": wavefront,
                           "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4)}
@@ -678,7 +670,7 @@ def main():
                                    "area lights (scene.hall_scene)"}[args.scene], "triangles": cs.n_tris,
               "width": W, "height": H, "spp_per_step": sps, "spp": spp, "max_depth": args.max_depth,
               "tile": args.tile, "parallelism": f"tile-split x{world}", "bvh_leaf": args.leaf,
-              "sah_isect": args.sah_isect, "builder": args.builder, "lookahead": la,
+              "sah_isect": args.sah_isect, "builder": args.builder,
               # the form the library ran (north_star names a wavefront; DESIGN.md §0 / §3.8 give the
               # measured reason for the persistent kernel on this scene) and the wavefront beside it
               "form": form["form"], "ordered_fetch": form["ordered"]}

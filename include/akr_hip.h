@@ -208,25 +208,20 @@ int akr_hip_create(int device, akr_hip_ctx **out);
 int akr_hip_destroy(akr_hip_ctx *ctx);
 const char *akr_hip_last_error(const akr_hip_ctx *ctx);
 /* Options: "stats" (per-kernel HIP-event timing: 0 off, 1 every kernel, 2 trace_closest only), "count_tests" (traversal counters),
- * "exact_cull", "wide", "lean", "shadow_grid_pct", "rays_per_lane" (tuning / A-B),
- * "lookahead" (speculative sample lanes per pixel, DESIGN.md §3.7: 1 = off (default), 0 = on
- * whenever "slot_target" gives a pixel two or more lanes, 2..64 = on with at most that many lanes;
- * results are identical for every value), "slot_target" (lookahead path slots per pass).
+ * "exact_cull", "wide", "lean", "shadow_grid_pct", "rays_per_lane" (tuning / A-B).
  * Render forms and their tuning (all give the same bits): "path" (0 wavefront,
  * 1 persistent kernel, 2 auto), "path_auto_pixels", "path_auto_complex";
  * the persistent form: "path_spec" (k_path_spec: 1 always, 0 never, 2 auto), "path_defer" (k_path_defer:
  * 1 forced, 0 k_path forced, 2 auto), the auto rule's "path_tail_ppl10" and "path_tail_steps" and its
  * overrides "path_spec_pixels", "path_defer_pixels", "path_defer_min_tris"; k_path_spec's "path_spec_depth",
- * "path_spec_alt", "path_spec_fetch", "path_spec_fetch_pixels";
+ * "path_spec_fetch", "path_spec_fetch_pixels";
  * "path_tab", "path_mix", "path_min_wait", "path_grid_pct", "path_prio";
  * the cost order: "path_order", "path_order_min_spp", "path_order_share_pixels", "path_order_share_min_spp",
  * "path_order_shift", "path_order_pair", "path_order_classes", "path_order_cap", "path_order_sub",
- * "path_order_pilot_spp", "wave_order" (the wavefront's camera rays in cost order); wavefront variants
- * (off by default, measured slower): "wave_dual" (two half-frame pipelines), "wave_stream"
- * (one streaming ray queue with per-slot sample regeneration).
+ * "path_order_pilot_spp", "wave_order" (the wavefront's camera rays in cost order).
  * "verify" (default 1): in-band film check after every render.  Test only: "pixel_probe" (record
  * akr_pixel_probe per slot), "fault_test" (raise the hang guard's fault word once), "ray_steps",
- * "serial_shadow", "any_far_first", "la_early_exit". */
+ * "serial_shadow", "any_far_first". */
 int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value);
 
 int akr_hip_upload_mesh(akr_hip_ctx *ctx, const float *vertices, uint64_t n_vertices,
@@ -323,20 +318,18 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
  * unpark with the new rays' start, and the shading's wait for the hit's record (out[19..22]).  Not part of the reference interface. */
 int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
-/* The last akr_hip_render's lookahead lanes per pixel and sample passes launched (diagnostic). */
+/* The last akr_hip_render's lanes per pixel (always 1) and sample passes launched (diagnostic). */
 int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes);
 /* Which form ran the last path render (all give the same bits): the wavefront
- * kernels (north_star's layout: raygen -> closest -> shade -> shadow -> splat launches), lookahead
- * lanes over the wavefront, the persistent path kernel, its deferred-NEE form or its speculative-sample
+ * kernels (north_star's layout: raygen -> closest -> shade -> shadow -> splat launches), the
+ * persistent path kernel, its deferred-NEE form or its speculative-sample
  * form; *ordered = 1 when
  * the persistent kernel fetched pixels in pilot-cost order.  AKR_FORM_NONE: nothing rendered. */
 #define AKR_FORM_NONE (-1)
 #define AKR_FORM_WAVEFRONT 0
-#define AKR_FORM_LOOKAHEAD 1
 #define AKR_FORM_PATH 2
 #define AKR_FORM_PATH_DEFER 3
 #define AKR_FORM_PATH_SPEC 4
-#define AKR_FORM_WAVE_STREAM 5 /* the wavefront's kernels over one streaming ray queue (option wave_stream) */
 int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered);
 /* The inputs of the last persistent render's form choice: its pixels per resident
  * lane x 1000, and the cost-ordering pilot's camera rays and their summed traversal steps; -1 when the

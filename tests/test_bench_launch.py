@@ -54,8 +54,7 @@ def test_roofline_traffic_only_from_a_profile_of_the_same_config(tmp_path):
     the line's config field for field: a 1-spp, unordered or whole-frame profile
     never stands in for the timed 1040-spp ordered launch or a rank's share."""
     cfg = {"workload": "C3", "triangles": 10_000_002, "width": 1920, "height": 1080, "spp_per_step": 52,
-           "spp": 1040, "form": "k_path", "ordered_fetch": True, "parallelism": "tile-split x1",
-           "lookahead": {"lanes": 1, "passes": 1}}
+           "spp": 1040, "form": "k_path", "ordered_fetch": True, "parallelism": "tile-split x1"}
     rec = {"hbm_bytes_per_spp": 11.5e9, "l2_req_bytes_per_spp": 40e9, "counters": {"VmemLatency": 900.0},
            "grid_threads": 262144}
     for tag, w in (("r01", cfg), ("r02", dict(cfg, ordered_fetch=False)), ("r03", dict(cfg, spp=20)),

@@ -158,7 +158,6 @@ def test_trace_each_ray_once(hip_ctx_factory, n):
         cs, orc = _setup(ctx, small_soup(20_000))
         rays = random_rays(n, 7, -1.1, 1.1)
         ctx.set_option("count_tests", 1)
-        ctx.set_option("lookahead", 1)   # no speculative lanes: exactly the sequential rays
         ctx.set_option("path_spec", 0)   # (k_path_spec's dropped samples trace rays too; its
         for any_hit in (False, True):    # committed rays are checked per pixel by the probe tests)
             ctx.reset_stats()
@@ -192,62 +191,28 @@ def _check_render(ctx, orc, spp, depth, tiles, W, H, clamp=0.0, exact=False, pro
     return rad, w
 
 
-@pytest.mark.parametrize("lookahead", [1, 0])
+@pytest.mark.parametrize("path", [0, 2])
 @pytest.mark.parametrize("exact", [False, True])
-def test_render_cornell_bit_exact(hip_ctx_factory, exact, lookahead):
+def test_render_cornell_bit_exact(hip_ctx_factory, exact, path):
+    """The Cornell box in the wavefront form (path 0) and the library's choice (path 2)."""
     with hip_ctx_factory(0) as ctx:
         cs, orc = _setup(ctx, cornell((64, 64)))
-        ctx.set_option("lookahead", lookahead)
+        ctx.set_option("path", path)
         rad, w = _check_render(ctx, orc, 16, 5, [(0, 0, 64, 64)], 64, 64, exact=exact)
         assert np.all(w == 16) and rad.mean() > 0
         info = ctx.render_info()
-        assert info["lanes"] == (1 if lookahead == 1 else 64)   # auto: the 64-lane cap for 4,096 pixels
-        assert info["passes"] <= 16
+        assert info["lanes"] == 1 and info["passes"] == (16 if path == 0 or exact else 1)
 
 
-@pytest.mark.parametrize("lookahead", [2, 3, 8, 64])
-def test_render_lookahead_bit_exact(hip_ctx_factory, lookahead):
-    """Lookahead lanes: lanes run the samples that start at planned draw offsets
-    from a pixel's committed sampler state; only the chain of lanes starting at real sample
-    boundaries is splatted, so every lane count gives the sequential image bit for bit.  spp not
-    divisible by the lanes, fewer samples than lanes, ragged tiles, depth 0 (every sample draws 4
-    numbers: all lanes accepted), depth 1/2/5 and the clamp."""
-    with hip_ctx_factory(0) as ctx:
-        cs, orc = _setup(ctx, cornell((40, 24)))
-        ctx.set_option("lookahead", lookahead)
-        tiles = [(0, 0, 16, 16), (24, 8, 40, 24), (30, 0, 64, 64), (5, 5, 5, 9)]
-        for spp, depth in ((13, 5), (2, 5), (7, 0), (5, 1), (9, 2)):
-            _check_render(ctx, orc, spp, depth, tiles, 40, 24)
-            info = ctx.render_info()
-            assert info["lanes"] == lookahead and info["passes"] <= spp
-            if depth == 0:   # constant sample length: the planned chain is all accepted
-                assert info["passes"] <= -(-spp // lookahead) + 2
-        _check_render(ctx, orc, 6, 5, tiles, 40, 24, clamp=10.0)
-        # repeated renders reuse the lane buffers (no state may leak from the previous render)
-        _check_render(ctx, orc, 11, 5, [(0, 0, 40, 24)], 40, 24)
-
-
-def test_render_lookahead_budget_growth(hip_ctx_factory):
-    """A slot budget of 1.6 pixels per pixel: 2 lanes per pixel while all are active, more lanes
-    per remaining pixel as pixels finish (the lane count per pass follows the active count)."""
-    with hip_ctx_factory(0) as ctx:
-        cs, orc = _setup(ctx, small_soup(50_000, (64, 36)))
-        ctx.set_option("lookahead", 0)
-        ctx.set_option("slot_target", int(1.6 * 64 * 36))
-        _check_render(ctx, orc, 16, 5, [(0, 0, 64, 36)], 64, 36)
-        info = ctx.render_info()
-        assert info["lanes"] == 2 and info["passes"] < 16
-
-
-def test_render_lookahead_soup_and_node(hip_ctx_factory):
+def test_render_soup_and_node_mixed_forms(hip_ctx_factory):
+    """A soup in both forms, and render_node over two contexts that run different forms: the same image."""
     with hip_ctx_factory(0) as ctx, hip_ctx_factory(0) as other:
         cs, orc = _setup(ctx, small_soup(50_000, (64, 36)))
-        for la in (1, 4):
-            ctx.set_option("lookahead", la)
+        for path in (0, 2):
+            ctx.set_option("path", path)
             _check_render(ctx, orc, 12, 5, [(0, 0, 64, 36)], 64, 36)
-        # render_node with a different lane count per context gives the same image
         scene.upload_scene(other, cs)
-        other.set_option("lookahead", 3)
+        other.set_option("path", 0)
         tiles = [(x, y, x + 16, y + 12) for y in range(0, 36, 12) for x in range(0, 64, 16)]
         ref, wref = ctx.render(7, 5, tiles, 64, 36)
         rad, w = capi.render_node([ctx, other], 7, 5, tiles, 64, 36)
@@ -608,7 +573,7 @@ def test_spec_and_order_options_are_validated(hip_ctx_factory):
                                ("path_order_pilot_spp", (0, 64), (-1, 65)), ("path_spec_fetch_pixels", (0, 1 << 40), (-1,)),
                                ("path_tail_ppl10", (0, 1 << 40), (-1,)), ("path_tail_steps", (0, 4096), (-1, 4097)), ("path_cache_mb", (0, 1 << 20), (-1,)),
                                ("leaf_align", (1, 8), (0, 3, 16)),
-                               ("wave_order", (0, 1), ()), ("path_spec_alt", (0, 1), ())):
+                               ("wave_order", (0, 1), ())):
             for v in good:
                 ctx.set_option(key, v)
             for v in bad:
@@ -704,14 +669,13 @@ def _tab_fits(cs):
                                                       (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
                                                       (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2),
                                                       (1, 2, 0, 1, 0), (1, 2, 0, 0, 2), (1, 2, 0, 1, 2),
-                                                      (1, 3, 0, 1, 0), (1, 3, 0, 1, 2), (1, 4, 0, 0, 0)])
+                                                      (1, 4, 0, 0, 0)])
 def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer, mix, tab, order):
     """The persistent path kernel (k_path), its deferred-NEE form (k_path_defer,
     §3.9: shadow rays handed to idle lanes of the wave, contributions added when the sample closes,
     scrambled or tile-order pixel fetch; defer = 1), its speculative-sample form (k_path_spec, §3.11:
     idle lanes run a busy pixel's next sample from a guessed sampler state, committed in order only
-    when the guess was the true state; defer = 2, 3 with the speculation tree's one-bounce branches, 4
-    with one sample beyond the head) and the wavefront kernels give the oracle's image bit for
+    when the guess was the true state; defer = 2, 4 with one sample beyond the head) and the wavefront kernels give the oracle's image bit for
     bit: ragged / clipped / empty tiles, depths 0-9 (above 8 the deferred form falls back to
     k_path), the clamp, Glossy + Mix + two-sided emitter, image textures, a soup whose rays take the
     deep stack, and a tile list smaller than one workgroup (fewer pixels than lanes); with the
@@ -722,7 +686,6 @@ def test_render_path_kernel_and_wavefront_bit_exact(hip_ctx_factory, path, defer
         ctx.set_option("path", path)
         ctx.set_option("path_defer", 1 if defer == 1 else 0)
         ctx.set_option("path_spec", 1 if defer >= 2 else 0)
-        ctx.set_option("path_spec_alt", 1 if defer == 3 else 0)
         ctx.set_option("path_spec_depth", 1 if defer == 4 else 3)
         ctx.set_option("path_mix", mix)
         ctx.set_option("path_tab", tab)
@@ -780,45 +743,30 @@ def test_cornell_gpu_render_matches_reference_ref_png(hip_ctx_factory, spp):
     assert gap_darker >= 8
 
 
-@pytest.mark.parametrize("order", [0, 1])
-def test_wavefront_dual_pipelines_bit_exact(hip_ctx_factory, order):
-    """The wavefront as two half-frame pipelines (option wave_dual, DESIGN.md §0: each half's raygen,
-    closest-hit / shade / shadow launches and splat on its own stream) renders the oracle's image bit
-    for bit, final sampler states and per-pixel ray counts included: Glossy / Mix, image textures and
-    a 100K soup, depths 0-5, ragged and overlapping tiles, with and without the cost-ordered camera
-    rays (order 1 forces the order at every spp)."""
+@pytest.mark.parametrize("bits,shadow", [(1, 0), (3, 1), (5, 2), (2, 2)])
+def test_wavefront_sorted_queues_bit_exact(hip_ctx_factory, bits, shadow):
+    """The wavefront with its extension-ray queues (and shadow queues: keyed by origin, 1, or end
+    point, 2) traced in the order of a spatial key (option wave_sort) renders the
+    oracle's image bit for bit, final sampler states and per-pixel ray counts included: Glossy / Mix,
+    image textures and a 100K soup, depths 0-5, ragged and overlapping tiles, the clamp, and the cost
+    order of the camera rays forced on at every spp."""
     for sc, W, H in ((mixed_scene((48, 48)), 48, 48), (textured_scene((48, 48)), 48, 48),
                      (small_soup(100_000, (96, 54)), 96, 54)):
         with hip_ctx_factory(0) as ctx:
             cs, orc = _setup(ctx, sc)
             ctx.set_option("path", 0)
-            ctx.set_option("wave_dual", 1)
-            ctx.set_option("path_order_min_spp", 0 if order else 10 ** 6)
-            ctx.set_option("path_order_share_min_spp", 0 if order else 10 ** 6)
+            ctx.set_option("wave_sort", bits)
+            ctx.set_option("wave_sort_shadow", shadow)
+            ctx.set_option("path_order_min_spp", 0)
+            ctx.set_option("path_order_share_min_spp", 0)
             tiles = [(0, 0, W, H), (5, 3, W - 7, H - 9), (W // 2, 0, W, H // 3)]
             for spp, depth in ((3, 5), (2, 0), (2, 1), (4, 2)):
                 _check_render(ctx, orc, spp, depth, tiles, W, H, probe=True)
-                assert ctx.render_form() == {"form": "wavefront", "ordered": bool(order)}
-
-
-@pytest.mark.parametrize("order", [0, 1])
-def test_wavefront_stream_bit_exact(hip_ctx_factory, order):
-    """The streaming wavefront (option wave_stream, DESIGN.md §0: one ray queue of every active slot's
-    current ray, whatever its bounce; a finished sample's next sample regenerated into the next
-    launch; splats after the sample's last shadow result) renders the oracle's image bit for bit,
-    final sampler states and per-pixel ray counts included: Glossy / Mix, image textures and a 100K
-    soup, depths 0-5 (with clamp), ragged and overlapping tiles, 1-9 spp, with and without the
-    cost-ordered first camera rays."""
-    for sc, W, H in ((mixed_scene((48, 48)), 48, 48), (textured_scene((48, 48)), 48, 48),
-                     (small_soup(100_000, (96, 54)), 96, 54)):
-        with hip_ctx_factory(0) as ctx:
-            cs, orc = _setup(ctx, sc)
-            ctx.set_option("path", 0)
-            ctx.set_option("wave_stream", 1)
-            ctx.set_option("path_order_min_spp", 0 if order else 10 ** 6)
-            ctx.set_option("path_order_share_min_spp", 0 if order else 10 ** 6)
-            tiles = [(0, 0, W, H), (5, 3, W - 7, H - 9), (W // 2, 0, W, H // 3)]
-            for spp, depth in ((3, 5), (2, 0), (1, 1), (4, 2), (9, 5)):
-                _check_render(ctx, orc, spp, depth, tiles, W, H, probe=True)
-                assert ctx.render_form() == {"form": "wavefront_stream", "ordered": bool(order)}
-            _check_render(ctx, orc, 5, 5, tiles, W, H, clamp=0.4, probe=True)
+                assert ctx.render_form() == {"form": "wavefront", "ordered": True}
+            _check_render(ctx, orc, 3, 5, tiles, W, H, clamp=0.4)
+    with hip_ctx_factory(0) as ctx:
+        for bad in (-1, 6):
+            with pytest.raises(capi.AkrError, match="wave_sort"):
+                ctx.set_option("wave_sort", bad)
+        with pytest.raises(capi.AkrError, match="wave_sort_shadow"):
+            ctx.set_option("wave_sort_shadow", 3)

@@ -23,6 +23,39 @@ def test_library_exports_every_declared_symbol():
     assert capi.load_library().akr_hip_api_version() == 3
 
 
+def test_product_build_compiles_no_probe_or_ab_variant():
+    """The product library is built from the Makefile's flags alone (no -D), and its sources hold no
+    timing probe or A/B build switch: an inexact probe (not bit-exact by design) can never be
+    compiled into libakr_hip.so.  Experiments live as patches under tools/experiments/ and build
+    into tools/experiments/lib/, the only place capi.load_library's override accepts."""
+    csrc = ROOT / "akarirender-1_amd" / "csrc"
+    mk = (csrc / "Makefile").read_text()
+    flags = [ln for ln in mk.splitlines() if ln.startswith(("FLAGS", "HIPCC", "\t$(HIPCC)", "\tg++"))]
+    assert flags and not any(re.search(r"(^|\s)-D", ln) for ln in flags), flags
+    assert "variant" not in mk
+    banned = re.compile(r"AKR_PROBE_(?!SEED|RAYS)|AKR_STACK16|AKR_PK_FMA|AKR_POP2|AKR_SPEC_PRIO|AKR_NEXT_SELECT|AKR_PATH_CALL_SHADE|"
+                        r"AKR_ROOT_SGPR|AKR_STREAM_DEBUG|AKR_ONE_POP")
+    for f in sorted(csrc.glob("*")):
+        if f.suffix in (".hip", ".h", ".cpp", ".hpp"):
+            hits = [i + 1 for i, ln in enumerate(f.read_text().splitlines()) if banned.search(ln)]
+            assert not hits, f"{f.name}: probe / A-B switch at lines {hits}"
+    # the only preprocessor conditionals left are the header guard of device code and tuning defaults
+    allowed = re.compile(r"#\s*(ifndef AKR_(TRACE_BLOCK|STACK_LDS|REFILL_MIN|REFILL_MIN_ANY|WHILE_EXIT|WHILE_EXIT_ANY|"
+                         r"WORK_SHARDS|TRACE_WAVES|PATH_WAVES|SHADE_BLOCK)\b|if defined\(__HIP_DEVICE_COMPILE__\)|"
+                         r"if defined\(__HIPCC__\)|ifdef __HIPCC__)")
+    for f in sorted(csrc.glob("*")):
+        if f.suffix in (".hip", ".h", ".cpp", ".hpp"):
+            for i, ln in enumerate(f.read_text().splitlines()):
+                if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b", ln):
+                    assert allowed.match(ln.strip()), f"{f.name}:{i + 1}: {ln.strip()}"
+    with pytest.raises(ImportError, match="tools/experiments"):
+        import subprocess, sys
+        r = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, 'akarirender-1_amd'); "
+                            "from akari_amd import capi"], cwd=ROOT, capture_output=True, text=True,
+                           env={**__import__("os").environ, "AKR_HIP_LIB": "/tmp/other.so"})
+        raise ImportError(r.stderr)
+
+
 def test_tile_arrays_pass_without_copy():
     """render calls take the tile list as an (n, 4) int32 array from capi.rect_array without a
     copy (the bench converts once, outside its timed region), or as a list of tuples."""

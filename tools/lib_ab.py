@@ -1,10 +1,10 @@
-"""A/B of library builds (make variant N=... D="-D..."; akarirender-1_amd/variants/libakr_hip_<N>.so) on
+"""A/B of library builds (tools/experiments/build.sh <name>: tools/experiments/lib/libakr_hip_<name>.so) on
 the C3 frame: the SBVH is built once (the product library) and saved under /tmp, then every build runs
 in its own process (AKR_HIP_LIB; one library per process, so no symbol of one build can bind to
 another's), adopting that BVH through akr_hip_import_accel, alternating builds for --repeat rounds.
 Each process times the whole frame and the given rank shares of an N-way split at --spp.
 
-Usage (GPU box): python tools/lib_ab.py --libs akarirender-1_amd/libakr_hip.so akarirender-1_amd/variants/libakr_hip_x.so
+Usage (GPU box): python tools/lib_ab.py --libs akarirender-1_amd/libakr_hip.so tools/experiments/lib/libakr_hip_x.so
                  [--spp 520] [--split 8 --ranks 0,5] [--repeat 2] [--opts key=v,...]"""
 import argparse
 import json

@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--tile", type=int, default=64, help="tile size of the split (bench.py's default; 32 before r20)")
     ap.add_argument("--configs", nargs="+", default=[""])
+    ap.add_argument("--kstats", type=int, default=0,
+                    help="N > 0: after the timed rounds, one N-spp render per config with HIP events on every "
+                         "launch, printing the per-kernel launch counts and average ms")
     ap.add_argument("--scene", choices=["soup", "cornell", "hall"], default="soup",
                     help="cornell: the C2 box at 1080p; hall: the C4 stand-in at 4K (ADVICE r4: wave_order there)")
     args = ap.parse_args()
@@ -102,6 +105,17 @@ def main():
                           "per_rank_min": {r: round(x, 4) for r, x in per.items()},
                           "max_over_ranks": round(max(per.values()), 4),
                           "all": {r: [round(x, 4) for x in v] for r, v in res[cfg].items()}}), flush=True)
+    if args.kstats:
+        for cfg, c in zip(args.configs, ctxs):
+            c.reset_stats()
+            c.set_option("stats", 1)
+            ms = run(c, shares[ranks[0]], args.kstats)
+            ks = c.kernel_stats()
+            c.set_option("stats", 0)
+            print(json.dumps({"kstats": cfg or "(defaults)", "spp": args.kstats, "ms_per_spp_with_events": round(ms, 4),
+                              "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4),
+                                              "ms_per_spp": round(v["total_ms"] / args.kstats, 4)}
+                                          for k, v in ks.items()}}), flush=True)
     for c in ctxs:
         c.close()
 
