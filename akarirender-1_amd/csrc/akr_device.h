@@ -296,6 +296,8 @@ struct PathArgs {
     uint32_t *fault;               // mapped host word: set when a wave stops on the hang guard (k_path_defer)
     uint32_t fault_test;           // test only: k_path_defer raises `fault` once at the end of the launch
     uint32_t spec_depth;           // k_path_spec: levels of the speculation tree (samples beyond the head)
+    const uint32_t *gate;          // optional: the launch exits at once unless *gate == gate_want (two
+    uint32_t gate_want;            //   candidate forms launched back to back, k_pick_form chose one)
     uint32_t probe_clock;          // diagnostic (counting build, option "pixel_probe" 2): the probe's flags
                                    // carry the pixel's completion time, (wall clock >> 4) << 8 | flags
 };

@@ -293,7 +293,11 @@ struct akr_hip_ctx {
     // rays and their summed steps
     int64_t last_ppl1000 = 0, last_pilot_rays = -1, last_pilot_steps = -1;
     DBuf<unsigned long long> d_steps_sum;   // the pilot's summed steps
-    uint32_t *h_sum = nullptr, *d_sum_host = nullptr;  // mapped host words it is copied into
+    DBuf<uint32_t> d_gate;                  // k_pick_form's choice between the two launched forms
+    // the last render launched two gated forms (gate_forms[gate]) / read the pilot's step sum on the
+    // device: resolved on the host by resolve_form() when the form or its inputs are queried
+    bool form_pending = false, pilot_sum_pending = false;
+    int32_t gate_forms[2] = {AKR_FORM_NONE, AKR_FORM_NONE};
     bool path_mix = true;     // option "path_mix": k_path_defer fetches pixels in scrambled order
     bool path_tab = true;     // option "path_tab": persistent kernels read the scene tables from an LDS copy
     // option "path_order": cost-ordered pixel fetch: a pilot camera ray per pixel
@@ -419,7 +423,6 @@ struct akr_hip_ctx {
         for (hipEvent_t e : {ev_fork, ev_join, ev_join_main, ev_shade[0], ev_shade[1], ev_shadow[0], ev_shadow[1], ev_splat[0], ev_splat[1]})
             if (e) (void)hipEventDestroy(e);
         if (h_check) (void)hipHostFree(h_check);
-        if (h_sum) (void)hipHostFree(h_sum);
         if (h_fault) (void)hipHostFree(h_fault);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_gather) (void)hipEventDestroy(ev_gather);
@@ -705,6 +708,7 @@ struct akr_hip_ctx {
         d_owork.reserve(kTraceWords);
         d_ocnt.reserve(3);
         d_steps_sum.reserve(1);
+        d_gate.reserve(1);
         d_otmp.reserve(pixel_order_tmp_bytes((uint32_t)std::min<size_t>(n, UINT32_MAX)));
         d_pprobe.reserve(n);  // the tail pilot's and the path pilot's probe (no allocation in a render)
         cap = n;
@@ -822,25 +826,22 @@ struct akr_hip_ctx {
         HIPCHK(hipMemsetAsync(d_film.p, 0, (size_t)N * sizeof(float4), ms));
     }
 
-    // The pilot's summed steps (pixel_order with sum_steps) on the host: the two words copied into
-    // mapped host memory, the host waiting for the render's stream once
-    uint64_t read_steps_sum(hipStream_t ms) {
-        if (!h_sum) {
-            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_sum), 2 * sizeof(uint32_t),
-                                 hipHostMallocMapped | hipHostMallocCoherent));
-            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_sum_host), h_sum, 0));
+    // The last render's form and pilot step sum, when they were left on the device (a gated launch):
+    // waits for that render, then reads the gate word and the sum
+    void resolve_form() {
+        if (!form_pending && !pilot_sum_pending) return;
+        if (done_recorded) HIPCHK(hipStreamWaitEvent(stream, ev_done, 0));
+        unsigned long long sum = 0;
+        uint32_t gate = 0;
+        HIPCHK(hipMemcpyAsync(&sum, d_steps_sum.p, sizeof(sum), hipMemcpyDeviceToHost, stream));
+        if (form_pending) HIPCHK(hipMemcpyAsync(&gate, d_gate.p, sizeof(gate), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        last_pilot_steps = (int64_t)sum;
+        if (form_pending) {
+            if (gate > 1) throw std::runtime_error("render form gate holds " + std::to_string(gate));
+            last_form = gate_forms[gate];
         }
-        volatile uint32_t *hv = reinterpret_cast<volatile uint32_t *>(h_sum);
-        hv[0] = hv[1] = kMappedSentinel;
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(d_steps_sum.p);
-        launch_store_word(w, d_sum_host, ms);
-        launch_store_word(w + 1, d_sum_host + 1, ms);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(ms));
-        const uint32_t lo = read_mapped(h_sum), hi = read_mapped(h_sum + 1);
-        if (lo == kMappedSentinel && hi == kMappedSentinel)
-            throw std::runtime_error("pilot: the device never reported its step sum");
-        return (uint64_t)lo | ((uint64_t)hi << 32);
+        form_pending = pilot_sum_pending = false;
     }
 
     // Path pilot (option path_order_pilot_spp): slots ranked by the rays their first S samples take
@@ -988,6 +989,7 @@ struct akr_hip_ctx {
         last_passes = 0;
         last_form = AKR_FORM_NONE;
         last_ordered = 0;
+        form_pending = pilot_sum_pending = false;
         probe_ok = false;
         probe_n = 0;
         const uint64_t N = setup_pixels(tiles, n_tiles, n_count_words, st);
@@ -1044,6 +1046,7 @@ struct akr_hip_ctx {
                 const int64_t ppl1000 = (int64_t)((N * 1000 + lanes / 2) / lanes);
                 last_ppl1000 = ppl1000;
                 last_pilot_rays = last_pilot_steps = -1;
+                form_pending = pilot_sum_pending = false;
                 // the first persistent render of a context runs the pilot once on a few pixels: its
                 // kernels (and rocPRIM's) are loaded then, not inside a later ordered render
                 if (path_order != 0 && !order_warm) {
@@ -1076,44 +1079,70 @@ struct akr_hip_ctx {
                         timed("pilot", ms, [&] { pixel_order((uint32_t)N, ms, want_steps); });
                     pa.order = d_oidx[1].p;
                 }
-                bool tail = false;
-                if (want_steps) {  // the host waits for the pilot (well under a millisecond at a rank share)
-                    const uint64_t rays = ((uint64_t)N + (1u << path_order_sub) - 1) >> path_order_sub;
-                    const uint64_t steps = read_steps_sum(ms);
-                    last_pilot_rays = (int64_t)rays;
-                    last_pilot_steps = (int64_t)steps;
-                    tail = steps >= (uint64_t)path_tail_steps * rays;
-                }
+                // The rule's tail test reads the pilot's step sum, which is on the device: no host wait
+                // inside the render.  k_pick_form writes a gate word from the sum, and both
+                // candidate kernels are launched back to back, each exiting at once unless the gate
+                // names it; the form that ran is read back only when akr_hip_render_form asks.
+                const int tail_kind = cache_resident ? PATH_DEFER
+                                                     : (path_spec == 2 ? PATH_SPEC : (p.max_depth <= 8 ? PATH_DEFER : PATH_PLAIN));
+                const bool gated = want_steps && tail_kind != PATH_PLAIN;
                 int kind = PATH_PLAIN;
                 if (path_spec == 1) kind = PATH_SPEC;
                 else if (path_defer == 1 && p.max_depth <= 8) kind = PATH_DEFER;
-                else if (path_defer == 2 && tail)
-                    kind = cache_resident ? PATH_DEFER
-                                    : (path_spec == 2 ? PATH_SPEC : (p.max_depth <= 8 ? PATH_DEFER : PATH_PLAIN));
-                const uint64_t resident = (uint64_t)path_grid[kind][tab] * (uint64_t)path_grid_pct / 100;
-                const uint32_t grid = (uint32_t)std::max<uint64_t>(
-                    1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
-                if (kind == PATH_DEFER) {
-                    d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
-                    pa.contrib = d_contrib.p;
-                    pa.mix = path_mix ? 1u : 0u;
+                // one candidate's launch arguments and grid
+                auto configure = [&](int k, PathArgs &x) {
+                    const uint64_t resident = (uint64_t)path_grid[k][tab] * (uint64_t)path_grid_pct / 100;
+                    const uint32_t grid = (uint32_t)std::max<uint64_t>(
+                        1, std::min<uint64_t>(resident, (N + kTraceBlock - 1) / kTraceBlock));
+                    if (k == PATH_DEFER) {
+                        d_contrib.reserve((size_t)18 * grid * kTraceBlock);  // 16 NEE slots + the waiting ray
+                        x.contrib = d_contrib.p;
+                        x.mix = path_mix ? 1u : 0u;
+                    }
+                    if (x.order && !(k == PATH_PLAIN || path_order == 2)) x.order = nullptr;  // path_order 1
+                    if (x.order) {
+                        const bool small = ppl1000 <= 1500;  // at most 1.5 pixels per resident lane (8-way share)
+                        const bool pair = path_order_pair == 3 ||
+                                          (k != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && small)));
+                        x.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
+                        // k_path_spec: every wave takes pixels from the whole cost order (FETCH_STRIDE), so
+                        // each has cheap pixels whose lanes turn helpers early (option path_spec_fetch)
+                        if (k == PATH_SPEC && path_spec_fetch >= 0 &&
+                            (path_spec_fetch_pixels > 0 ? (int64_t)N <= path_spec_fetch_pixels : small))
+                            x.order_mode = (uint32_t)path_spec_fetch;
+                        x.prio = (uint32_t)path_prio;
+                    }
+                    return grid;
+                };
+                auto form_of = [](int k) {
+                    return k == PATH_SPEC ? AKR_FORM_PATH_SPEC : (k == PATH_DEFER ? AKR_FORM_PATH_DEFER : AKR_FORM_PATH);
+                };
+                if (want_steps) last_pilot_rays = (int64_t)(((uint64_t)N + (1u << path_order_sub) - 1) >> path_order_sub);
+                if (gated) {
+                    launch_pick_form(d_steps_sum.p, (unsigned long long)path_tail_steps * (uint64_t)last_pilot_rays,
+                                     d_gate.p, ms);
+                    PathArgs p0 = pa, p1 = pa;
+                    const uint32_t g0 = configure(PATH_PLAIN, p0), g1 = configure(tail_kind, p1);
+                    p0.gate = p1.gate = d_gate.p;
+                    p0.gate_want = 0u;
+                    p1.gate_want = 1u;
+                    timed("path", ms, [&] {  // one timed record: the launch that exits at once adds microseconds
+                        launch_path(count, PATH_PLAIN, tab, p0, g0, ms);
+                        launch_path(count, tail_kind, tab, p1, g1, ms);
+                    });
+                    HIPCHK(hipGetLastError());
+                    gate_forms[0] = form_of(PATH_PLAIN);
+                    gate_forms[1] = form_of(tail_kind);
+                    form_pending = true;
+                    last_form = AKR_FORM_NONE;
+                    pa.order = p0.order;
+                } else {
+                    if (want_steps) pilot_sum_pending = true;  // the step sum is read back on request
+                    const uint32_t grid = configure(kind, pa);
+                    timed("path", ms, [&] { launch_path(count, kind, tab, pa, grid, ms); });
+                    HIPCHK(hipGetLastError());
+                    last_form = form_of(kind);
                 }
-                if (pa.order && !(kind == PATH_PLAIN || path_order == 2)) pa.order = nullptr;  // path_order 1
-                if (pa.order) {
-                    const bool small = ppl1000 <= 1500;  // at most 1.5 pixels per resident lane (8-way share)
-                    const bool pair = path_order_pair == 3 ||
-                                      (kind != PATH_PLAIN && (path_order_pair == 1 || (path_order_pair == 2 && small)));
-                    pa.order_mode = pair ? 2u : 0u;  // FETCH_PAIR / FETCH_LINEAR
-                    // k_path_spec: every wave takes pixels from the whole cost order (FETCH_STRIDE), so
-                    // each has cheap pixels whose lanes turn helpers early (option path_spec_fetch)
-                    if (kind == PATH_SPEC && path_spec_fetch >= 0 &&
-                        (path_spec_fetch_pixels > 0 ? (int64_t)N <= path_spec_fetch_pixels : small))
-                        pa.order_mode = (uint32_t)path_spec_fetch;
-                    pa.prio = (uint32_t)path_prio;
-                }
-                timed("path", ms, [&] { launch_path(count, kind, tab, pa, grid, ms); });
-                HIPCHK(hipGetLastError());
-                last_form = kind == PATH_SPEC ? AKR_FORM_PATH_SPEC : (kind == PATH_DEFER ? AKR_FORM_PATH_DEFER : AKR_FORM_PATH);
                 last_ordered = pa.order ? 1 : 0;
             }
             last_passes = 1;
@@ -2205,6 +2234,7 @@ int akr_hip_render_info(akr_hip_ctx *ctx, int32_t *lanes, int32_t *passes) {
 
 int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered) {
     return guard(ctx, [&] {
+        ctx->resolve_form();
         if (form) *form = ctx->last_form;
         if (ordered) *ordered = ctx->last_ordered;
     });
@@ -2213,6 +2243,7 @@ int akr_hip_render_form(akr_hip_ctx *ctx, int32_t *form, int32_t *ordered) {
 int akr_hip_render_form_inputs(akr_hip_ctx *ctx, int64_t *pixels_per_lane_x1000, int64_t *pilot_rays,
                                int64_t *pilot_steps) {
     return guard(ctx, [&] {
+        ctx->resolve_form();
         if (pixels_per_lane_x1000) *pixels_per_lane_x1000 = ctx->last_ppl1000;
         if (pilot_rays) *pilot_rays = ctx->last_pilot_rays;
         if (pilot_steps) *pilot_steps = ctx->last_pilot_steps;

@@ -1717,6 +1717,7 @@ constexpr int kParkSlots = 8;
 
 template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path(PathArgs pa) {
+    if (pa.gate && *pa.gate != pa.gate_want) return;  // the other candidate form runs (uniform: before any barrier)
     const TraceArgs &a = pa.t;
     __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
@@ -1995,6 +1996,7 @@ struct DeferState {
 
 template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_defer(PathArgs pa) {
+    if (pa.gate && *pa.gate != pa.gate_want) return;  // the other candidate form runs (uniform: before any barrier)
     const TraceArgs &a = pa.t;
     __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
@@ -2341,6 +2343,7 @@ struct SpecState {
 
 template <bool COUNT, bool TAB>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR_PATH_WAVES))) void k_path_spec(PathArgs pa) {
+    if (pa.gate && *pa.gate != pa.gate_want) return;  // the other candidate form runs (uniform: before any barrier)
     const TraceArgs &a = pa.t;
     __shared__ unsigned long long s_stack_mem[kStackLdsU64];
     __shared__ uint32_t s_park[kParkSlots][kTraceBlock];
@@ -2824,6 +2827,12 @@ __global__ __launch_bounds__(kBlock) void k_probe_seed(const uint32_t *seed, uin
     probe[i] = q;
 }
 
+// The form rule's tail test on the device: gate = 1 when the pilot's camera rays
+// took at least `thresh` traversal steps in all
+__global__ void k_pick_form(const unsigned long long *sum, unsigned long long thresh, uint32_t *gate) {
+    if (threadIdx.x == 0) *gate = *sum >= thresh ? 1u : 0u;
+}
+
 __global__ void k_store_word(const uint32_t *src, uint32_t *dst) {
     if (threadIdx.x == 0) {
         __atomic_store_n(dst, *src, __ATOMIC_RELAXED);
@@ -2890,6 +2899,9 @@ void launch_sort(const SortArgs &a, uint32_t max_items, hipStream_t st) {
     hipLaunchKernelGGL(k_sort_keys, grid, dim3(kBlock), 0, st, a);
     hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanBlock), 0, st, a);
     hipLaunchKernelGGL(k_sort_place, grid, dim3(kBlock), 0, st, a);
+}
+void launch_pick_form(const unsigned long long *sum, unsigned long long thresh, uint32_t *gate, hipStream_t st) {
+    hipLaunchKernelGGL(k_pick_form, dim3(1), dim3(64), 0, st, sum, thresh, gate);
 }
 void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st) {
     hipLaunchKernelGGL(k_store_word, dim3(1), dim3(64), 0, st, src, dst);
