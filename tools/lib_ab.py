@@ -4,6 +4,7 @@ in its own process (AKR_HIP_LIB; one library per process, so no symbol of one bu
 another's), adopting that BVH through akr_hip_import_accel, alternating builds for --repeat rounds.
 Each process times the whole frame and the given rank shares of an N-way split at --spp.
 
+A library may carry options of its own after an "@" (path@key=v,key=v), added to --opts.
 Usage (GPU box): python tools/lib_ab.py --libs akarirender-1_amd/libakr_hip.so tools/experiments/lib/libakr_hip_x.so
                  [--spp 520] [--split 8 --ranks 0,5] [--repeat 2] [--opts key=v,...]"""
 import argparse
@@ -77,9 +78,11 @@ def main():
     try:
         for rep in range(args.repeat):
             for lib in args.libs:
-                env = dict(os.environ, AKR_HIP_LIB=str(Path(lib).resolve()))
+                path, _, own = lib.partition("@")
+                env = dict(os.environ, AKR_HIP_LIB=str(Path(path).resolve()))
+                opts = ",".join(x for x in (args.opts, own) if x)
                 cmd = [sys.executable, __file__, "--worker", "--spp", str(args.spp), "--split", str(args.split),
-                       "--ranks", args.ranks, "--tris", str(args.tris), "--opts", args.opts, "--bvh", args.bvh]
+                       "--ranks", args.ranks, "--tris", str(args.tris), "--opts", opts, "--bvh", args.bvh]
                 p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
                 line = next((l for l in p.stdout.splitlines() if l.startswith("RESULT ")), None)
                 if p.returncode != 0 or line is None:
