@@ -177,7 +177,8 @@ struct SortArgs {
     uint32_t *perm;                // out: sorted position -> entry
     float lo[3], scale[3];         // cell = (p - lo) * scale, clamped to [0, 2^bits)
     uint32_t bits;                 // Morton bits per axis
-    uint32_t nbins;                // 2^(3 bits + 3)
+    uint32_t octant;               // the direction octant below the cell (3 more key bits)
+    uint32_t nbins;                // 2^(3 bits + 3 octant) <= 4096
     uint32_t end_point;            // key point: o + d * tmax (finite tmax) instead of o
 };
 

@@ -346,7 +346,8 @@ struct akr_hip_ctx {
     bool wave_order = true;
     // option "wave_sort": the wavefront's extension-ray queues traced in the order of a spatial key
     // (DESIGN.md §3.3): the Morton cell of the ray origin in a 2^wave_sort grid per axis over the scene
-    // box, then the direction octant (0 = off, 1..5 bits per axis); option "wave_sort_shadow": the shadow
+    // box, then the direction octant while the key fits 12 bits (0 = off, 1..4 bits per axis; 4: the
+    // cell alone); option "wave_sort_shadow": the shadow
     // queues too, keyed by their origin on the light (1) or by the shaded point they end at (2)
     int wave_sort = 0;
     int wave_sort_shadow = 0;
@@ -1171,10 +1172,11 @@ struct akr_hip_ctx {
         // ray reordering (option wave_sort): [0] the extension queues on the main stream, [1] the shadow
         // queues on the side stream, each with its own keys, histogram and cursors
         const int sbits = wave_sort > 0 ? wave_sort : 3;
+        const bool soct = 3 * sbits + 3 <= 12;  // the octant below the cell while the key fits 12 bits
         const bool sort_ext = wave_sort > 0 && nb > 1, sort_sh = wave_sort_shadow > 0 && p.max_depth > 0;
         SortArgs sa[2] = {};
         if (sort_ext || sort_sh) {
-            const uint32_t nbins = 1u << (3 * sbits + 3);
+            const uint32_t nbins = 1u << (3 * sbits + (soct ? 3 : 0));
             for (int q = 0; q < 2; q++) {
                 if (q == 0 ? !sort_ext : !sort_sh) continue;
                 d_skey[q].reserve(N);
@@ -1188,6 +1190,7 @@ struct akr_hip_ctx {
                 x.hist = d_shist[q].p;
                 x.cursor = d_scursor[q].p;
                 x.bits = (uint32_t)sbits;
+                x.octant = soct ? 1u : 0u;
                 x.nbins = nbins;
                 x.end_point = q == 1 && wave_sort_shadow == 2 ? 1u : 0u;
                 for (int k = 0; k < 3; k++) {
@@ -1514,7 +1517,7 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
         } else if (k == "wave_order") {
             ctx->wave_order = value != 0;
         } else if (k == "wave_sort") {
-            if (value < 0 || value > 5) throw std::runtime_error("wave_sort must be in [0, 5] (Morton bits per axis, 0 = off)");
+            if (value < 0 || value > 4) throw std::runtime_error("wave_sort must be in [0, 4] (Morton bits per axis, 0 = off)");
             ctx->wave_sort = (int)value;
         } else if (k == "wave_sort_shadow") {
             if (value < 0 || value > 2) throw std::runtime_error("wave_sort_shadow must be 0, 1 (origin) or 2 (end point)");

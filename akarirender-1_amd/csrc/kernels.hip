@@ -820,40 +820,36 @@ __device__ __forceinline__ uint32_t sort_key(const SortArgs &a, float4 r0, float
         const int q = f >= 0.0f ? (f < (float)g ? (int)f : g - 1) : 0;  // NaN -> 0
         c[k] = (uint32_t)q;
     }
+    const uint32_t cell = spread3(c[0]) | (spread3(c[1]) << 1) | (spread3(c[2]) << 2);
+    if (!a.octant) return cell;
     const uint32_t oct = (r1.x > 0.0f ? 1u : 0u) | (r1.y > 0.0f ? 2u : 0u) | (r1.z > 0.0f ? 4u : 0u);
-    return ((spread3(c[0]) | (spread3(c[1]) << 1) | (spread3(c[2]) << 2)) << 3) | oct;
+    return (cell << 3) | oct;
 }
 
-// One atomic per distinct key of a wave (the queue is coherent after the first sorted bounce, so a
-// wave holds few keys): the lanes of each key add their count at once.  Returns the lane's position
-// among the lanes of its key plus the value the atomic returned.
-__device__ __forceinline__ uint32_t wave_bin_add(bool active, uint32_t key, uint32_t *ctr) {
-    uint32_t out = 0;
-    unsigned long long left = __ballot(active);
-    while (left) {
-        const int leader = __ffsll((long long)left) - 1;
-        const uint32_t lk = (uint32_t)__shfl((int)key, leader);
-        const unsigned long long m = __ballot(active && key == lk);
-        uint32_t base = 0;
-        if ((int)__lane_id() == leader) base = atomicAdd(ctr + lk, (uint32_t)__popcll(m));
-        base = (uint32_t)__shfl((int)base, leader);
-        if (active && key == lk) out = base + lane_prefix(m);
-        left &= ~m;
-    }
-    return out;
-}
+// Both passes count a block's 4,096 entries in an LDS histogram first and touch the global
+// histogram / cursors once per distinct key of the block: the sorted queues are coherent, so one
+// global atomic per entry would serialise every wave of a region on the same few bins.
+constexpr int kSortItems = 16;                        // entries per thread
+constexpr int kSortTile = kSortItems * kBlock;        // entries per workgroup
+constexpr uint32_t kSortMaxBins = 4096;               // 12 key bits (LDS: 16 KB per workgroup)
 
 __global__ __launch_bounds__(kBlock) void k_sort_keys(SortArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = *a.count;
-    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup
-    const bool act = i < n;
-    uint32_t k = 0;
-    if (act) {
-        k = sort_key(a, a.rays[2 * (size_t)i], a.rays[2 * (size_t)i + 1]);
-        a.key[i] = k;
+    __shared__ uint32_t s_cnt[kSortMaxBins];
+    const uint32_t n = *a.count, base = blockIdx.x * kSortTile;
+    if (base >= n) return;  // uniform per workgroup
+    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock) s_cnt[b] = 0u;
+    __syncthreads();
+    for (int k = 0; k < kSortItems; k++) {
+        const uint32_t i = base + (uint32_t)k * kBlock + threadIdx.x;
+        if (i < n) {
+            const uint32_t key = sort_key(a, a.rays[2 * (size_t)i], a.rays[2 * (size_t)i + 1]);
+            a.key[i] = key;
+            atomicAdd(&s_cnt[key], 1u);
+        }
     }
-    (void)wave_bin_add(act, k, a.hist);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock)
+        if (s_cnt[b]) atomicAdd(&a.hist[b], s_cnt[b]);
 }
 
 // One workgroup: cursor = exclusive prefix of hist, hist = 0 for the next sort
@@ -881,13 +877,24 @@ __global__ __launch_bounds__(kScanBlock) void k_sort_scan(SortArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_sort_place(SortArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = *a.count;
-    if (blockIdx.x * kBlock >= n) return;  // uniform per workgroup
-    const bool act = i < n;
-    const uint32_t k = act ? a.key[i] : 0u;
-    const uint32_t pos = wave_bin_add(act, k, a.cursor);
-    if (act) a.perm[pos] = i;
+    __shared__ uint32_t s_pos[kSortMaxBins];
+    const uint32_t n = *a.count, base = blockIdx.x * kSortTile;
+    if (base >= n) return;  // uniform per workgroup
+    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock) s_pos[b] = 0u;
+    __syncthreads();
+    for (int k = 0; k < kSortItems; k++) {
+        const uint32_t i = base + (uint32_t)k * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&s_pos[a.key[i]], 1u);
+    }
+    __syncthreads();
+    // the block's range of each bin, then each entry's place in it
+    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock)
+        if (s_pos[b]) s_pos[b] = atomicAdd(&a.cursor[b], s_pos[b]);
+    __syncthreads();
+    for (int k = 0; k < kSortItems; k++) {
+        const uint32_t i = base + (uint32_t)k * kBlock + threadIdx.x;
+        if (i < n) a.perm[atomicAdd(&s_pos[a.key[i]], 1u)] = i;
+    }
 }
 
 // ------------------------------------------------------------------------------------ raygen
@@ -2895,7 +2902,8 @@ void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
 }
 void launch_sort(const SortArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
-    const dim3 grid(blocks_for(max_items));
+    if (a.nbins > kSortMaxBins) throw std::runtime_error("launch_sort: at most 4096 key bins");
+    const dim3 grid((uint32_t)((max_items + kSortTile - 1) / kSortTile));
     hipLaunchKernelGGL(k_sort_keys, grid, dim3(kBlock), 0, st, a);
     hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanBlock), 0, st, a);
     hipLaunchKernelGGL(k_sort_place, grid, dim3(kBlock), 0, st, a);

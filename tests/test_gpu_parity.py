@@ -743,7 +743,7 @@ def test_cornell_gpu_render_matches_reference_ref_png(hip_ctx_factory, spp):
     assert gap_darker >= 8
 
 
-@pytest.mark.parametrize("bits,shadow", [(1, 0), (3, 1), (5, 2), (2, 2)])
+@pytest.mark.parametrize("bits,shadow", [(1, 0), (3, 1), (4, 2), (2, 2)])
 def test_wavefront_sorted_queues_bit_exact(hip_ctx_factory, bits, shadow):
     """The wavefront with its extension-ray queues (and shadow queues: keyed by origin, 1, or end
     point, 2) traced in the order of a spatial key (option wave_sort) renders the
@@ -765,7 +765,7 @@ def test_wavefront_sorted_queues_bit_exact(hip_ctx_factory, bits, shadow):
                 assert ctx.render_form() == {"form": "wavefront", "ordered": True}
             _check_render(ctx, orc, 3, 5, tiles, W, H, clamp=0.4)
     with hip_ctx_factory(0) as ctx:
-        for bad in (-1, 6):
+        for bad in (-1, 5):
             with pytest.raises(capi.AkrError, match="wave_sort"):
                 ctx.set_option("wave_sort", bad)
         with pytest.raises(capi.AkrError, match="wave_sort_shadow"):

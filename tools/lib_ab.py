@@ -47,6 +47,14 @@ def worker(args):
         torch.cuda.synchronize(dev)
         out[name] = round((time.perf_counter() - t) / args.spp * 1e3, 4)
         out[name + " form"] = ctx.render_form()["form"] + " ppl %.2f" % ctx.render_form_inputs()["pixels_per_lane"]
+        if args.kstats:   # one more render with HIP events on every launch: per-kernel ms per spp
+            ctx.reset_stats()
+            ctx.set_option("stats", 1)
+            ctx.render_device(args.kstats, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
+            torch.cuda.synchronize(dev)
+            ctx.set_option("stats", 0)
+            out[name + " kstats"] = {k: [v["launches"], round(v["total_ms"] / args.kstats, 4)]
+                                     for k, v in ctx.kernel_stats().items()}
     ctx.close()
     print("RESULT " + json.dumps(out), flush=True)
 
@@ -60,6 +68,7 @@ def main():
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--opts", default="")
+    ap.add_argument("--kstats", type=int, default=0, help="N > 0: per-kernel launches and ms per spp of an N-spp render")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--bvh", default="/tmp/akr_lib_ab_bvh")
     args = ap.parse_args()
@@ -82,7 +91,8 @@ def main():
                 env = dict(os.environ, AKR_HIP_LIB=str(Path(path).resolve()))
                 opts = ",".join(x for x in (args.opts, own) if x)
                 cmd = [sys.executable, __file__, "--worker", "--spp", str(args.spp), "--split", str(args.split),
-                       "--ranks", args.ranks, "--tris", str(args.tris), "--opts", opts, "--bvh", args.bvh]
+                       "--ranks", args.ranks, "--tris", str(args.tris), "--opts", opts, "--bvh", args.bvh,
+                       "--kstats", str(args.kstats)]
                 p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
                 line = next((l for l in p.stdout.splitlines() if l.startswith("RESULT ")), None)
                 if p.returncode != 0 or line is None:
@@ -96,7 +106,7 @@ def main():
             Path(args.bvh + suf).unlink(missing_ok=True)
     print("summary (min over repeats, ms per spp)", flush=True)
     for lib, rs in res.items():
-        keys = [k for k in rs[0] if not k.endswith(" form")]
+        keys = [k for k in rs[0] if not k.endswith((" form", " kstats"))]
         print(json.dumps({"lib": lib, **{k: min(r[k] for r in rs) for k in keys}}), flush=True)
 
 
