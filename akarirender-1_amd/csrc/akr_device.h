@@ -271,6 +271,7 @@ struct PathProfile {
     // with the splat, pixel fetch and camera ray, and the unpark with the new rays' start
     unsigned long long tp_park, tp_next, tp_begin;
     unsigned long long tp_load;    // of t_shade: until the hit's shading record is loaded
+    unsigned long long leaf_phases, leaf_holders;  // leaf phases with a leaf held, lanes holding one (summed per wave)
 };
 
 // Persistent path kernel (k_path): the whole sample loop of every pixel of the tile list.

@@ -2223,7 +2223,8 @@ int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n) {
         if (ctx->d_pprof.p) HIPCHK(hipMemcpy(&q, ctx->d_pprof.p, sizeof(q), hipMemcpyDeviceToHost));
         const uint64_t v[] = {q.waves, q.outer, q.procs, q.trav_iters, q.t_proc, q.t_trav, q.t_leaf, q.t_total, q.t_max,
                               q.lanes_proc, q.t_shade, q.spec_started, q.spec_aborted, q.tv_issue, q.tv_wait,
-                              q.tv_comp, q.tl_issue, q.tl_wait, q.tl_comp, q.tp_park, q.tp_next, q.tp_begin, q.tp_load};
+                              q.tv_comp, q.tl_issue, q.tl_wait, q.tl_comp, q.tp_park, q.tp_next, q.tp_begin, q.tp_load,
+                              q.leaf_phases, q.leaf_holders};
         for (int32_t k = 0; k < n && k < (int32_t)(sizeof(v) / sizeof(v[0])); k++) out[k] = v[k];
     });
 }

@@ -1373,6 +1373,8 @@ struct PathCount {
     // loads, waiting for them (an explicit vmcnt(0) wait between two clock reads), the dependent
     // work after they return (slot tests, stack, ballots; leaf box and triangle loop)
     unsigned long long tv_issue = 0, tv_wait = 0, tv_comp = 0, tl_issue = 0, tl_wait = 0, tl_comp = 0;
+    // leaf phases entered with at least one lane holding a leaf, and those lanes summed
+    unsigned long long lphases = 0, lholders = 0;
     bool deep_now = false;
 };
 
@@ -1512,6 +1514,9 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
         bool hit_any = false;
         const unsigned long long ta = wall_clock64();
         const bool in_leaf = busy && r.leaf != AKR_CHILD_EMPTY;
+        const uint32_t holders = (uint32_t)__popcll(__ballot(in_leaf));
+        c.lphases += holders ? 1u : 0u;
+        c.lholders += holders;
         // every lane loads (a lane without a leaf the blob's first record: see path_traverse)
         const float4 *lr = wide_leaves + (in_leaf ? (r.leaf & 0x7FFFFFFFu) : 0u);
         const float4 l0 = lr[0], l1 = lr[1], pa0 = lr[2], pb0 = lr[3], pc0 = lr[4], pa1 = lr[5], pb1 = lr[6],
@@ -1680,6 +1685,8 @@ __device__ __forceinline__ void path_count_flush(const PathArgs &pa, PathCount &
         atomicAdd(&q.tl_issue, c.tl_issue);
         atomicAdd(&q.tl_wait, c.tl_wait);
         atomicAdd(&q.tl_comp, c.tl_comp);
+        atomicAdd(&q.leaf_phases, c.lphases);
+        atomicAdd(&q.leaf_holders, c.lholders);
     }
     const int slot_of[2] = {TRACE_CLOSEST, TRACE_SHADOW};
     for (int m = 0; m < 2; m++) {

@@ -154,7 +154,9 @@ def time_split(pp, counts):
            "leaf": {"total": f(pp["t_leaf"]), "issue": f(pp["tl_issue"]), "wait": f(pp["tl_wait"]), "work": f(pp["tl_comp"])},
            "other": f(tot - pp["t_proc"] - pp["t_trav"] - pp["t_leaf"]),
            "lanes": {"traversal_busy": round((cl["visits"] + sh["visits"]) / max(1, cl["slots_traversal"]), 4),
-                     "triangle_loop": round((cl["tri_tests"] + sh["tri_tests"]) / max(1, cl["slots_tri"]), 4)},
+                     "triangle_loop": round((cl["tri_tests"] + sh["tri_tests"]) / max(1, cl["slots_tri"]), 4),
+                     # lanes holding a leaf when a wave enters its leaf phase (of 64), VERDICT r5 item 6
+                     "leaf_phase_holders": round(pp.get("leaf_holders", 0) / max(1, pp.get("leaf_phases", 0)), 2)},
            "iterations_per_wave": round(pp["trav_iters"] / max(1, pp["waves"]), 1),
            # the launch lasts as long as its longest wave: the ratio to the mean wave is the launch's tail
            "longest_wave_over_mean": round(pp["t_max"] * pp["waves"] / tot, 4) if pp.get("waves") else None,

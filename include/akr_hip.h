@@ -315,7 +315,9 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
  * results (shading), k_path_spec's speculative samples started / dropped, and the time split of the
  * traversal and leaf phases: ticks issuing their loads, waiting for them, working after them, then
  * k_path's processing split: the park, the sample end with splat / pixel fetch / camera ray, and the
- * unpark with the new rays' start, and the shading's wait for the hit's record (out[19..22]).  Not part of the reference interface. */
+ * unpark with the new rays' start, and the shading's wait for the hit's record (out[19..22]),
+ * then the leaf phases entered with a leaf held and the lanes holding one, summed (out[23..24]).
+ * Not part of the reference interface. */
 int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
 /* The last akr_hip_render's lanes per pixel (always 1) and sample passes launched (diagnostic). */

@@ -47,6 +47,20 @@ def worker(args):
         torch.cuda.synchronize(dev)
         out[name] = round((time.perf_counter() - t) / args.spp * 1e3, 4)
         out[name + " form"] = ctx.render_form()["form"] + " ppl %.2f" % ctx.render_form_inputs()["pixels_per_lane"]
+        if args.count:   # a 1-spp counting pass: lane utilisation of the loops, lanes holding a leaf per leaf phase
+            ctx.set_option("count_tests", 1)
+            ctx.reset_stats()
+            ctx.render_device(1, 5, tiles, film[:3 * n].data_ptr(), film[3 * n:4 * n].data_ptr(), stream)
+            torch.cuda.synchronize(dev)
+            ctx.set_option("count_tests", 0)
+            cl, sh = (ctx.trace_counts()["per_mode"][m] for m in ("closest", "shadow"))
+            pp = ctx.path_profile()
+            out[name + " lanes"] = {
+                "traversal": round((cl["visits"] + sh["visits"]) / max(1, cl["slots_traversal"]), 4),
+                "triangles": round((cl["tri_tests"] + sh["tri_tests"]) / max(1, cl["slots_tri"]), 4),
+                "holders_per_leaf_phase": round(pp["leaf_holders"] / max(1, pp["leaf_phases"]), 2),
+                "holding_ray": round(cl["slots_busy"] / max(1, cl["slots_traversal"]), 4)}
+            ctx.reset_stats()
         if args.kstats:   # one more render with HIP events on every launch: per-kernel ms per spp
             ctx.reset_stats()
             ctx.set_option("stats", 1)
@@ -69,6 +83,7 @@ def main():
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--opts", default="")
     ap.add_argument("--kstats", type=int, default=0, help="N > 0: per-kernel launches and ms per spp of an N-spp render")
+    ap.add_argument("--count", action="store_true", help="also a 1-spp counting pass (lane utilisation)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--bvh", default="/tmp/akr_lib_ab_bvh")
     args = ap.parse_args()
@@ -92,7 +107,7 @@ def main():
                 opts = ",".join(x for x in (args.opts, own) if x)
                 cmd = [sys.executable, __file__, "--worker", "--spp", str(args.spp), "--split", str(args.split),
                        "--ranks", args.ranks, "--tris", str(args.tris), "--opts", opts, "--bvh", args.bvh,
-                       "--kstats", str(args.kstats)]
+                       "--kstats", str(args.kstats)] + (["--count"] if args.count else [])
                 p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
                 line = next((l for l in p.stdout.splitlines() if l.startswith("RESULT ")), None)
                 if p.returncode != 0 or line is None:
@@ -106,7 +121,7 @@ def main():
             Path(args.bvh + suf).unlink(missing_ok=True)
     print("summary (min over repeats, ms per spp)", flush=True)
     for lib, rs in res.items():
-        keys = [k for k in rs[0] if not k.endswith((" form", " kstats"))]
+        keys = [k for k in rs[0] if not k.endswith((" form", " kstats", " lanes"))]
         print(json.dumps({"lib": lib, **{k: min(r[k] for r in rs) for k in keys}}), flush=True)
 
 
