@@ -162,24 +162,6 @@ struct TraceArgs {                 // kept small: fewer SGPRs, higher residency
     uint32_t *ray_steps;           // COUNT builds, diagnostic: per ray, traversal iterations + triangle tests
     uint32_t step_cap;             // COUNT builds with ray_steps: a ray stops after this many steps (0: none;
                                    // the cost-ordered fetch's pilot, whose hits nobody reads)
-    const uint32_t *perm;          // optional: fetch position -> queue entry (the wavefront's ray order,
-                                   // option wave_sort); results go to the entry's own index
-};
-
-// Reordering of a wavefront ray queue by a spatial key (option wave_sort): a counting
-// sort of the entries' indices by (Morton cell of the key point in the scene box, direction octant)
-struct SortArgs {
-    const float4 *rays;            // the queue's records (o | tmin, d | tmax)
-    const uint32_t *count;         // its length (device)
-    uint32_t *key;                 // per entry
-    uint32_t *hist;                // [nbins]: zero before k_sort_keys; k_sort_scan zeroes it again
-    uint32_t *cursor;              // [nbins]: each bin's next free sorted position
-    uint32_t *perm;                // out: sorted position -> entry
-    float lo[3], scale[3];         // cell = (p - lo) * scale, clamped to [0, 2^bits)
-    uint32_t bits;                 // Morton bits per axis
-    uint32_t octant;               // the direction octant below the cell (3 more key bits)
-    uint32_t nbins;                // 2^(3 bits + 3 octant) <= 4096
-    uint32_t end_point;            // key point: o + d * tmax (finite tmax) instead of o
 };
 
 struct ShadeArgs {

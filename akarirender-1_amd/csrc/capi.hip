@@ -198,7 +198,6 @@ struct akr_hip_ctx {
     DBuf<float4> d_wleaves;          // leaf blob (see TraceArgs::wide_leaves)
     uint32_t wide_root_dev = AKR_CHILD_EMPTY;
     uint64_t bvh_dev_bytes = 0;       // the uploaded wide nodes + leaf blob
-    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // root box (wavefront ray keys)
     DBuf<float4> d_tris;
     DBuf<ShadeTri> d_shade_tri;
     DBuf<float> d_tc, d_images, d_cdf, d_func;
@@ -272,8 +271,9 @@ struct akr_hip_ctx {
     // option "path_cache_mb": a BVH of at most this many MiB on the device (wide nodes + leaf blob) is
     // taken as cache-resident (half the 256-MiB Infinity Cache: the kernel streams its film and rays
     // beside it, MI355X_MICROARCH.md §Infinity Cache): its rule form is k_path_defer at every size
-    // (soups of 100K triangles, ~15 MB: 4-20 % faster than k_path; 1M, ~150 MB, and 10M, ~1.5 GB, take
-    // k_path_spec on rank shares)
+    // (the SBVH of a 100K-triangle soup is 10.7 MiB and of a 1M soup 109.8 MiB: both cache-resident,
+    // k_path_defer 4-20 % faster than k_path there; the 10M soup's 1.5 GB tree takes k_path_spec on
+    // rank shares)
     int64_t path_cache_mb = 128;
     // explicit overrides of the rule's size test (0, default: pixels per lane): a tail form for renders
     // of at most this many pixels (options "path_spec_pixels", "path_defer_pixels"); option
@@ -344,14 +344,6 @@ struct akr_hip_ctx {
     // option "wave_order": the wavefront's camera rays queued in the cost order (costliest first in
     // each shard of the closest-hit launch), by the same rule and floors as the persistent kernels
     bool wave_order = true;
-    // option "wave_sort": the wavefront's extension-ray queues traced in the order of a spatial key
-    // (DESIGN.md §3.3): the Morton cell of the ray origin in a 2^wave_sort grid per axis over the scene
-    // box, then the direction octant while the key fits 12 bits (0 = off, 1..4 bits per axis; 4: the
-    // cell alone); option "wave_sort_shadow": the shadow
-    // queues too, keyed by their origin on the light (1) or by the shaded point they end at (2)
-    int wave_sort = 0;
-    int wave_sort_shadow = 0;
-    DBuf<uint32_t> d_skey[2], d_shist[2], d_scursor[2], d_sperm_ext, d_sperm_sh[2];
     DBuf<uint4> d_pprobe;  // the path pilot's per-slot probe
     DBuf<uint32_t> d_okey[2], d_oidx[2], d_owork;
     DBuf<uint8_t> d_otmp;
@@ -1169,40 +1161,6 @@ struct akr_hip_ctx {
             }
             last_ordered = worder ? 1 : 0;
         }
-        // ray reordering (option wave_sort): [0] the extension queues on the main stream, [1] the shadow
-        // queues on the side stream, each with its own keys, histogram and cursors
-        const int sbits = wave_sort > 0 ? wave_sort : 3;
-        const bool soct = 3 * sbits + 3 <= 12;  // the octant below the cell while the key fits 12 bits
-        const bool sort_ext = wave_sort > 0 && nb > 1, sort_sh = wave_sort_shadow > 0 && p.max_depth > 0;
-        SortArgs sa[2] = {};
-        if (sort_ext || sort_sh) {
-            const uint32_t nbins = 1u << (3 * sbits + (soct ? 3 : 0));
-            for (int q = 0; q < 2; q++) {
-                if (q == 0 ? !sort_ext : !sort_sh) continue;
-                d_skey[q].reserve(N);
-                if (d_shist[q].n < nbins) {
-                    d_shist[q].reserve(nbins);
-                    HIPCHK(hipMemsetAsync(d_shist[q].p, 0, nbins * sizeof(uint32_t), ms));  // k_sort_scan re-zeroes it
-                }
-                d_scursor[q].reserve(nbins);
-                SortArgs &x = sa[q];
-                x.key = d_skey[q].p;
-                x.hist = d_shist[q].p;
-                x.cursor = d_scursor[q].p;
-                x.bits = (uint32_t)sbits;
-                x.octant = soct ? 1u : 0u;
-                x.nbins = nbins;
-                x.end_point = q == 1 && wave_sort_shadow == 2 ? 1u : 0u;
-                for (int k = 0; k < 3; k++) {
-                    x.lo[k] = scene_lo[k];
-                    const float ext = scene_hi[k] - scene_lo[k];
-                    x.scale[k] = ext > 0.0f ? (float)(1 << sbits) / ext : 0.0f;
-                }
-            }
-            if (sort_ext) d_sperm_ext.reserve(N);
-            if (sort_sh)
-                for (int k = 0; k < 2; k++) d_sperm_sh[k].reserve(N);
-        }
         for (int s = 0; s < p.spp; s++) {
             const int ps = s & 1;
             last_passes++;
@@ -1225,7 +1183,6 @@ struct akr_hip_ctx {
                 t.rays = odd ? d_ray1.p : d_ray0.p;
                 t.count = qcount(b);
                 t.hits = d_hit.p;
-                t.perm = sort_ext && b > 0 ? d_sperm_ext.p : nullptr;  // the camera rays keep the tile / cost order
                 timed("trace_closest", ms, [&] { trace_launch(TRACE_CLOSEST, tight, t, N, ms); });
                 // shade refills shadow queue g % 2: the shadow trace of bounce g - 2 must be done
                 if (g >= 2) HIPCHK(hipStreamWaitEvent(ms, ev_shadow[sq], 0));
@@ -1252,24 +1209,8 @@ struct akr_hip_ctx {
                 timed("shade", ms, [&] { launch_shade(sh, (uint32_t)N, ms); });
                 HIPCHK(hipEventRecord(ev_shade[sq], ms));
                 HIPCHK(hipStreamWaitEvent(side, ev_shade[sq], 0));
-                if (sort_ext && b + 1 < nb) {  // the next bounce's queue, in key order
-                    SortArgs x = sa[0];
-                    x.rays = sh.ray_out;
-                    x.count = qcount(b + 1);
-                    x.perm = d_sperm_ext.p;
-                    timed("sort", ms, [&] { launch_sort(x, (uint32_t)N, ms); });
-                }
                 if (b < p.max_depth) {
-                    if (sort_sh) {
-                        SortArgs x = sa[1];
-                        x.rays = d_sray[sq].p;
-                        x.count = scount(b);
-                        x.perm = d_sperm_sh[sq].p;
-                        hipStream_t sst = serial_shadow ? ms : side;
-                        timed("sort_shadow", sst, [&] { launch_sort(x, (uint32_t)N, sst); });
-                    }
                     TraceArgs ts = trace_args(work(b, 1));
-                    ts.perm = sort_sh ? d_sperm_sh[sq].p : nullptr;
                     ts.stack_ovf = d_ovf_side.p;  // concurrent with a main-stream trace
                     ts.rays = d_sray[sq].p;
                     ts.count = scount(b);
@@ -1516,12 +1457,6 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->path_spec = (int)value;
         } else if (k == "wave_order") {
             ctx->wave_order = value != 0;
-        } else if (k == "wave_sort") {
-            if (value < 0 || value > 4) throw std::runtime_error("wave_sort must be in [0, 4] (Morton bits per axis, 0 = off)");
-            ctx->wave_sort = (int)value;
-        } else if (k == "wave_sort_shadow") {
-            if (value < 0 || value > 2) throw std::runtime_error("wave_sort_shadow must be 0, 1 (origin) or 2 (end point)");
-            ctx->wave_sort_shadow = (int)value;
         } else if (k == "path_order_pilot_spp") {
             if (value < 0 || value > 64) throw std::runtime_error("path_order_pilot_spp must be in [0, 64]");
             ctx->path_order_pilot_spp = (int)value;
@@ -1757,17 +1692,6 @@ void finish_accel(akr_hip_ctx *ctx, int n_threads) {
         ctx->d_wleaves.upload(blob.get(), words + pad, ctx->stream);
         // the uploaded tree's bytes (the DBufs' capacities only grow), for the form rule
         ctx->bvh_dev_bytes = (uint64_t)wn.size() * sizeof(akr_bvh4_node) + (uint64_t)(words + pad) * sizeof(float4);
-        // the scene box (the virtual root's child 0: the real root's box) for the wavefront's ray keys
-        for (int k = 0; k < 3; k++) ctx->scene_lo[k] = ctx->scene_hi[k] = 0.0f;
-        if (!b.nodes.empty()) {
-            const akr_bvh_node &r = b.nodes[0];
-            const float lo[3] = {r.bxy0[0], r.bxy0[2], r.bz[0]}, hi[3] = {r.bxy0[1], r.bxy0[3], r.bz[1]};
-            for (int k = 0; k < 3; k++)
-                if (std::isfinite(lo[k]) && std::isfinite(hi[k]) && hi[k] >= lo[k]) {
-                    ctx->scene_lo[k] = lo[k];
-                    ctx->scene_hi[k] = hi[k];
-                }
-        }
         HIPCHK(hipStreamSynchronize(ctx->stream));  // before the host staging vectors go away
         ctx->d_tris.upload(reinterpret_cast<const float4 *>(b.tris.data()), 3 * b.tris.size(), ctx->stream);
         HIPCHK(hipStreamSynchronize(ctx->stream));

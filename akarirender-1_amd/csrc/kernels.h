@@ -14,8 +14,6 @@ int trace_blocks_per_cu(int mode);
 void launch_raygen(const RaygenArgs &a, hipStream_t st);
 void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st);
 void launch_splat(const SplatArgs &a, uint32_t max_items, hipStream_t st);
-// wavefront ray order (option wave_sort): keys + histogram, scan, placement of the queue's entries
-void launch_sort(const SortArgs &a, uint32_t max_items, hipStream_t st);
 void launch_pick_form(const unsigned long long *sum, unsigned long long thresh, uint32_t *gate, hipStream_t st);
 void launch_store_word(const uint32_t *src, uint32_t *dst, hipStream_t st);
 void launch_ao_shade(const AoShadeArgs &a, uint32_t max_items, hipStream_t st);

@@ -579,9 +579,9 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                 if (!busy) {
                     const uint32_t my = first + lane_prefix(idle);
                     if (my < s_hi && base < s_hi - s_lo) {
-                        idx = a.perm ? a.perm[my] : my;  // the sorted order's entry (option wave_sort)
-                        ra = a.rays[2 * (size_t)idx];
-                        rb = a.rays[2 * (size_t)idx + 1];
+                        idx = my;
+                        ra = a.rays[2 * (size_t)my];
+                        rb = a.rays[2 * (size_t)my + 1];
                         fresh = true;
                     }
                 }
@@ -788,112 +788,6 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
             atomicAdd(&a.counters[MODE].deep, c_deep);
             atomicAdd(&a.counters[MODE].leaves, c_leaf);
         }
-    }
-}
-
-// ------------------------------------------------------------------------------ ray reordering
-// Option wave_sort: before a closest-hit or shadow trace of the wavefront, the
-// queue's entries are ordered by a key — the Morton code of the ray's key point in a 2^bits grid over
-// the scene box, then its direction octant — so the lanes of a wave, and the waves of one XCD (its
-// shard of the queue), walk the same subtrees.  A counting sort of indices: the trace reads entry
-// perm[j] at position j and writes its result at the entry's own index, so nothing downstream moves
-// and every result is the unsorted one (each ray's traversal is independent of its neighbours).
-__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // bit i -> bit 3 i (v < 2^10)
-    v = (v | (v << 16)) & 0x030000FFu;
-    v = (v | (v << 8)) & 0x0300F00Fu;
-    v = (v | (v << 4)) & 0x030C30C3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-__device__ __forceinline__ uint32_t sort_key(const SortArgs &a, float4 r0, float4 r1) {
-    float p[3] = {r0.x, r0.y, r0.z};
-    if (a.end_point && isfinite(r1.w)) {
-        p[0] = r0.x + r1.x * r1.w;
-        p[1] = r0.y + r1.y * r1.w;
-        p[2] = r0.z + r1.z * r1.w;
-    }
-    const int g = 1 << a.bits;
-    uint32_t c[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const float f = (p[k] - a.lo[k]) * a.scale[k];
-        const int q = f >= 0.0f ? (f < (float)g ? (int)f : g - 1) : 0;  // NaN -> 0
-        c[k] = (uint32_t)q;
-    }
-    const uint32_t cell = spread3(c[0]) | (spread3(c[1]) << 1) | (spread3(c[2]) << 2);
-    if (!a.octant) return cell;
-    const uint32_t oct = (r1.x > 0.0f ? 1u : 0u) | (r1.y > 0.0f ? 2u : 0u) | (r1.z > 0.0f ? 4u : 0u);
-    return (cell << 3) | oct;
-}
-
-// Both passes count a block's 4,096 entries in an LDS histogram first and touch the global
-// histogram / cursors once per distinct key of the block: the sorted queues are coherent, so one
-// global atomic per entry would serialise every wave of a region on the same few bins.
-constexpr int kSortItems = 16;                        // entries per thread
-constexpr int kSortTile = kSortItems * kBlock;        // entries per workgroup
-constexpr uint32_t kSortMaxBins = 4096;               // 12 key bits (LDS: 16 KB per workgroup)
-
-__global__ __launch_bounds__(kBlock) void k_sort_keys(SortArgs a) {
-    __shared__ uint32_t s_cnt[kSortMaxBins];
-    const uint32_t n = *a.count, base = blockIdx.x * kSortTile;
-    if (base >= n) return;  // uniform per workgroup
-    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock) s_cnt[b] = 0u;
-    __syncthreads();
-    for (int k = 0; k < kSortItems; k++) {
-        const uint32_t i = base + (uint32_t)k * kBlock + threadIdx.x;
-        if (i < n) {
-            const uint32_t key = sort_key(a, a.rays[2 * (size_t)i], a.rays[2 * (size_t)i + 1]);
-            a.key[i] = key;
-            atomicAdd(&s_cnt[key], 1u);
-        }
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock)
-        if (s_cnt[b]) atomicAdd(&a.hist[b], s_cnt[b]);
-}
-
-// One workgroup: cursor = exclusive prefix of hist, hist = 0 for the next sort
-constexpr int kScanBlock = 1024;
-__global__ __launch_bounds__(kScanBlock) void k_sort_scan(SortArgs a) {
-    __shared__ uint32_t s_sum[kScanBlock];
-    const uint32_t per = (a.nbins + kScanBlock - 1) / kScanBlock, b0 = threadIdx.x * per;
-    uint32_t tot = 0;
-    for (uint32_t b = b0; b < b0 + per && b < a.nbins; b++) tot += a.hist[b];
-    s_sum[threadIdx.x] = tot;
-    __syncthreads();
-    for (int off = 1; off < kScanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t v = threadIdx.x >= (uint32_t)off ? s_sum[threadIdx.x - off] : 0u;
-        __syncthreads();
-        s_sum[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = s_sum[threadIdx.x] - tot;
-    for (uint32_t b = b0; b < b0 + per && b < a.nbins; b++) {
-        const uint32_t h = a.hist[b];
-        a.cursor[b] = run;
-        a.hist[b] = 0u;
-        run += h;
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_sort_place(SortArgs a) {
-    __shared__ uint32_t s_pos[kSortMaxBins];
-    const uint32_t n = *a.count, base = blockIdx.x * kSortTile;
-    if (base >= n) return;  // uniform per workgroup
-    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock) s_pos[b] = 0u;
-    __syncthreads();
-    for (int k = 0; k < kSortItems; k++) {
-        const uint32_t i = base + (uint32_t)k * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&s_pos[a.key[i]], 1u);
-    }
-    __syncthreads();
-    // the block's range of each bin, then each entry's place in it
-    for (uint32_t b = threadIdx.x; b < a.nbins; b += kBlock)
-        if (s_pos[b]) s_pos[b] = atomicAdd(&a.cursor[b], s_pos[b]);
-    __syncthreads();
-    for (int k = 0; k < kSortItems; k++) {
-        const uint32_t i = base + (uint32_t)k * kBlock + threadIdx.x;
-        if (i < n) a.perm[atomicAdd(&s_pos[a.key[i]], 1u)] = i;
     }
 }
 
@@ -2906,14 +2800,6 @@ void launch_shade(const ShadeArgs &a, uint32_t max_items, hipStream_t st) {
     if (max_items == 0) return;
     const dim3 grid((uint32_t)((max_items + kShadeBlock - 1) / kShadeBlock));
     hipLaunchKernelGGL(k_shade, grid, dim3(kShadeBlock), 0, st, a);
-}
-void launch_sort(const SortArgs &a, uint32_t max_items, hipStream_t st) {
-    if (max_items == 0) return;
-    if (a.nbins > kSortMaxBins) throw std::runtime_error("launch_sort: at most 4096 key bins");
-    const dim3 grid((uint32_t)((max_items + kSortTile - 1) / kSortTile));
-    hipLaunchKernelGGL(k_sort_keys, grid, dim3(kBlock), 0, st, a);
-    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanBlock), 0, st, a);
-    hipLaunchKernelGGL(k_sort_place, grid, dim3(kBlock), 0, st, a);
 }
 void launch_pick_form(const unsigned long long *sum, unsigned long long thresh, uint32_t *gate, hipStream_t st) {
     hipLaunchKernelGGL(k_pick_form, dim3(1), dim3(64), 0, st, sum, thresh, gate);

@@ -665,6 +665,31 @@ def _tab_fits(cs):
     return nl * 96 + nm * 48 + (nl + 1) * 4 <= 1024
 
 
+def test_form_rule_reads_the_uploaded_tree_size(hip_ctx_factory):
+    """The rule's cache-resident test sizes the tree the context holds now: after a
+    rebuild into a smaller tree the render takes the cache-resident form, whatever the device buffers'
+    capacities kept from the larger tree."""
+    cs = scene.compile_scene(small_soup(200_000, (48, 27)))
+
+    def dev_bytes(builder):   # wide nodes + leaf blob as the library uploads them (align 1, 3 float4 of padding)
+        *_, (wn, lv, _) = capi.build_bvh_host(cs.vertices, cs.indices, builder=builder, n_threads=1, wide=True)
+        return len(wn) * 64 + (int(np.sum(2 + 3 * lv["count"].astype(np.int64))) + 3) * 16
+
+    big, small = dev_bytes(capi.BUILDER_SBVH), dev_bytes(capi.BUILDER_SAH)   # SBVH references are duplicated
+    mib = (small >> 20) + 1                  # a cache share between the two trees
+    assert small <= mib << 20 < big, (small, big)
+    with hip_ctx_factory(0) as ctx:
+        scene.upload_scene(ctx, cs, builder=capi.BUILDER_SBVH, n_threads=1)
+        ctx.set_option("path_tail_steps", 1)
+        ctx.set_option("path_cache_mb", mib)
+        tiles = [(0, 0, 48, 27)]
+        ctx.render(16, 5, tiles, 48, 27)
+        assert ctx.render_form()["form"] == "k_path_spec"     # the large tree: not cache-resident
+        ctx.build_accel(builder=capi.BUILDER_SAH, n_threads=1)
+        ctx.render(16, 5, tiles, 48, 27)
+        assert ctx.render_form()["form"] == "k_path_defer"    # the small one is
+
+
 @pytest.mark.parametrize("path,defer,mix,tab,order", [(0, 0, 0, 1, 0), (0, 0, 0, 1, 1), (1, 0, 0, 0, 0), (1, 0, 0, 1, 0),
                                                       (1, 0, 0, 1, 1), (1, 1, 0, 1, 0), (1, 1, 1, 0, 0),
                                                       (1, 1, 1, 1, 0), (1, 1, 1, 1, 2), (1, 0, 0, 1, 2),
@@ -741,32 +766,3 @@ def test_cornell_gpu_render_matches_reference_ref_png(hip_ctx_factory, spp):
           f"gap blocks darker: {gap_darker}/10")
     assert frac >= 0.99, fails
     assert gap_darker >= 8
-
-
-@pytest.mark.parametrize("bits,shadow", [(1, 0), (3, 1), (4, 2), (2, 2)])
-def test_wavefront_sorted_queues_bit_exact(hip_ctx_factory, bits, shadow):
-    """The wavefront with its extension-ray queues (and shadow queues: keyed by origin, 1, or end
-    point, 2) traced in the order of a spatial key (option wave_sort) renders the
-    oracle's image bit for bit, final sampler states and per-pixel ray counts included: Glossy / Mix,
-    image textures and a 100K soup, depths 0-5, ragged and overlapping tiles, the clamp, and the cost
-    order of the camera rays forced on at every spp."""
-    for sc, W, H in ((mixed_scene((48, 48)), 48, 48), (textured_scene((48, 48)), 48, 48),
-                     (small_soup(100_000, (96, 54)), 96, 54)):
-        with hip_ctx_factory(0) as ctx:
-            cs, orc = _setup(ctx, sc)
-            ctx.set_option("path", 0)
-            ctx.set_option("wave_sort", bits)
-            ctx.set_option("wave_sort_shadow", shadow)
-            ctx.set_option("path_order_min_spp", 0)
-            ctx.set_option("path_order_share_min_spp", 0)
-            tiles = [(0, 0, W, H), (5, 3, W - 7, H - 9), (W // 2, 0, W, H // 3)]
-            for spp, depth in ((3, 5), (2, 0), (2, 1), (4, 2)):
-                _check_render(ctx, orc, spp, depth, tiles, W, H, probe=True)
-                assert ctx.render_form() == {"form": "wavefront", "ordered": True}
-            _check_render(ctx, orc, 3, 5, tiles, W, H, clamp=0.4)
-    with hip_ctx_factory(0) as ctx:
-        for bad in (-1, 5):
-            with pytest.raises(capi.AkrError, match="wave_sort"):
-                ctx.set_option("wave_sort", bad)
-        with pytest.raises(capi.AkrError, match="wave_sort_shadow"):
-            ctx.set_option("wave_sort_shadow", 3)

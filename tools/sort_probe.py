@@ -1,8 +1,9 @@
-"""The wavefront's ray reordering (option wave_sort) measured per scene:
+"""The wavefront's ray reordering (tools/experiments/wave_sort.patch: option wave_sort; run with
+AKR_HIP_LIB=tools/experiments/lib/libakr_hip_wave_sort.so) measured per scene:
 for each configuration, one context at a time (one context per process time: several live contexts share
 the process's four hardware queues and serialise their streams), the BVH imported from one SBVH build,
 ms per spp of a render in the production stream layout, then a 1-spp counting pass for the traversal
-loop's lane utilisation and the node visits per ray.  --pmc-config runs only that configuration, for a
+loop's lane utilisation and the node visits per ray.  --no-count with one configuration is the form for a
 rocprofv3 --pmc pass around it (tools/sort_pmc.py sums the trace kernels' counters).
 
 Usage (GPU box): python tools/sort_probe.py --scene soup [--spp 32] [--split 8 --rank 0]

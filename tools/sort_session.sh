@@ -1,4 +1,5 @@
 export TMPDIR=/tmp
+export AKR_HIP_LIB=$PWD/tools/experiments/lib/libakr_hip_wave_sort.so   # tools/experiments/build.sh wave_sort
 S="python -u tools/sort_probe.py"
 PMC="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"
 tools/gpu_session.sh \
