@@ -16,6 +16,8 @@
 #          waves' total and waiting cycles: what the non-VMEM waits are
 #   mix    instruction mix per wave (VALU / SALU / branch / LDS / VMEM / SMEM)
 #   tcp    L1 (TCP) stall cycles (pending misses, data path to TA, tag conflicts) and its accesses
+# The counter passes skip the untimed side legs (the CPU baseline, the C2 / C4 legs and the wavefront leg):
+# their timed launch is the same, and the passes stay short.
 # tools/prof_summary.py <tag> turns gpurun_out/prof_<tag>/ into profiles/<tag>_{summary.md,traffic.json}.
 # Usage (GPU box, repo root): [PASSES="rq rq2"] tools/profile_driver.sh <tag> [bench args]
 tag=${1:-drv}; shift
@@ -46,7 +48,7 @@ for name in $passes; do
             python3 bench.py $args > "$out/kt.log" 2>&1
     else
         timeout -s KILL 240 rocprofv3 --pmc ${PMC[$name]} --kernel-trace --output-format csv -d "$out/$name" -o run -- \
-            python3 bench.py $args --cpu-baseline 0 > "$out/$name.log" 2>&1
+            python3 bench.py $args --cpu-baseline 0 --side-legs 0 --wavefront-spp 0 > "$out/$name.log" 2>&1
     fi
     rc=$?
     echo "pass $name rc=$rc" | tee -a "$out/progress.txt"
