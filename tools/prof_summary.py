@@ -176,17 +176,10 @@ def main(tag):
                        f"{c['TCC_EA0_RDREQ_LEVEL_sum'] / c['TCC_EA0_RDREQ_sum']:.0f} cycles per request")
     (dst / f"{tag}_traffic.json").write_text(json.dumps(
         {"tag": tag, "command": f"python3 bench.py {args}", "workload": workload,
-         "source": f"profiles/{tag}_*.csv (tools/profile_driver.sh)", "kernels": kernels}, indent=1) + "\n")
+         "source": f"rocprofv3 passes of tools/profile_driver.sh {tag} (the raw counter csvs stay under gpurun_out/; "
+                   "the per-launch counters the summary uses are in this file)", "kernels": kernels}, indent=1) + "\n")
     (dst / f"{tag}_summary.md").write_text("\n".join(out) + "\n")
     shutil.copy(src / "kt" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
-    for sub in PASSES:
-        f = src / sub / "run_counter_collection.csv"
-        if f.exists():
-            # only the akr kernels' rows (the runtime's copy kernels make the files large)
-            rows = [r for r in csv.reader(open(f))]
-            keep = [rows[0]] + [r for r in rows[1:] if any("akr::" in x for x in r)]
-            with open(dst / f"{tag}_{sub}.csv", "w", newline="") as fo:
-                csv.writer(fo).writerows(keep)
     print((dst / f"{tag}_summary.md").read_text())
 
 
