@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--min-wait", default="0", help="0: the per-kernel default (comma list)")
     ap.add_argument("--path", default="1")
     ap.add_argument("--far-first", default="0", help="occlusion rays far slots first (comma list)")
-    ap.add_argument("--defer", default="2", help="path_defer: 0 k_path, 1 k_path_defer at every size, 2 the library's choice (comma list; r18 sweeps ran with 1, DESIGN.md §9 caveat)")
+    ap.add_argument("--defer", default="2", help="path_defer: 0 k_path, 1 k_path_defer at every size, 2 the library's choice (comma list; r18 sweeps ran with 1, EXPERIMENTS.md §9 caveat)")
     ap.add_argument("--mix", default="1", help="scrambled pixel fetch in k_path_defer (comma list)")
     ap.add_argument("--grid-pct", default="100", help="persistent path grid, %% of resident (comma list)")
     ap.add_argument("--tab", default="1", help="scene tables in LDS (comma list)")
