@@ -2373,6 +2373,55 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 }
             }
             if (COUNT) p_tsh += wall_clock64() - p_ts;
+            // Until a lane of the wave finds the pixel queue drained no lane can be a helper: every group
+            // is its owner alone, running its head.  Steps 2-5 then reduce to k_path's processing: commit
+            // a finished head, fetch a pixel, start the next head from C, without the group bookkeeping.
+            const bool fast = !__any(done);
+            if (fast) {
+                bool head = false;  // start the head sample from C
+                if (s.role() == ROLE_OWNER && s.send()) {  // Tile::add_sample, C = the head's end state
+                    float4 fm = pa.film[pix];
+                    splat_one(fm, make_float4(Lr.x, Lr.y, Lr.z, 0.0f), pa.ray_clamp);
+                    pa.film[pix] = fm;
+                    if (COUNT) {
+                        pc_closest += sc_closest;
+                        pc_shadow += sc_shadow;
+                    }
+                    C = seed;
+                    cseq++;
+                    occ = 0;
+                    s.set(SpecState::SEND, 1, 0);
+                    if (cseq == spp) {
+                        if (pa.probe)
+                            pa.probe[pix] = make_uint4(C, COUNT ? pc_closest : 0u, COUNT ? pc_shadow : 0u, probe_flags<COUNT>(pa));
+                        s.set(SpecState::ROLE, 2, ROLE_FREE);
+                        s.set(SpecState::NH, 5, 0);
+                        grp = 0;
+                    } else {
+                        head = true;
+                    }
+                }
+                bool need = s.role() == ROLE_FREE && !done;
+                const bool asked = need;
+                fetch_pixels(f, n, pa.work, pa.order ? pa.order_mode : FETCH_LINEAR, pa.order, pa.prio, need, done, pix);
+                if (asked && !need) {
+                    const uint32_t px = pa.pixel[pix];
+                    C = (uint32_t)((int)(px & 0xFFFFu) + (int)(px >> 16) * pa.cam.width);
+                    cseq = 0;
+                    occ = 0;
+                    grp = 1ull << lane;
+                    s.set(SpecState::ROLE, 2, ROLE_OWNER);
+                    s.set(SpecState::NH, 5, 0);
+                    if (COUNT) pc_closest = pc_shadow = 0;
+                    head = true;
+                }
+                if (head) {
+                    seed = C;
+                    occ |= 1u;
+                    s.set(SpecState::NODE, 4, 0);
+                    start = true;
+                }
+            } else {
             // 2. commits, in sample order: a finished head is committed and its length picks the
             // branch of the tree that moves up; rounds until no group has a finished head
             const int ol = s.role() == ROLE_HELPER ? (int)s.ol() : (int)lane;
@@ -2550,6 +2599,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                         start = true;
                     }
                 }
+            }
+            }  // general path
+            {
                 if (start) {  // a new sample: camera ray (pathtracer.h:61-64), L = 0, beta = 1
                     const uint32_t px = pa.pixel[pix];  // reloaded: a register shuffled to the helpers measured slower (profiles/r21_px_reg_spec_ab.log)
                     Lr = V3{0.0f, 0.0f, 0.0f};
