@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--configs", nargs="+", default=["path=0", "path=0,wave_sort=3"])
     ap.add_argument("--no-count", action="store_true", help="skip the counting pass (PMC runs)")
+    ap.add_argument("--kstats", type=int, default=0, help="N > 0: per-kernel ms per spp of an N-spp render with HIP events")
     args = ap.parse_args()
     import torch
     from akari_amd import capi, dist, scene
@@ -85,6 +86,12 @@ def main():
                               "lane_util_traversal": round(x["visits"] / max(1, x["slots_traversal"]), 4),
                               "holding_ray": round(x["slots_busy"] / max(1, x["slots_traversal"]), 4),
                               "lane_util_triangles": round(x["tri_tests"] / max(1, x["slots_tri"]), 4)}
+            if args.kstats:
+                c.reset_stats()
+                c.set_option("stats", 1)
+                render(c, args.kstats)
+                c.set_option("stats", 0)
+                rec["kstats"] = {k: [v["launches"], round(v["total_ms"] / args.kstats, 4)] for k, v in c.kernel_stats().items()}
             print("SORT " + json.dumps(rec), flush=True)
 
 
