@@ -136,6 +136,17 @@ __device__ __forceinline__ void block_append2(bool want_a, uint32_t *ctr_a, uint
 }
 
 // ------------------------------------------------------------------------------------- trace
+// The leaf phase's triangle records are loaded with the leaf's header in one batch (EXPERIMENTS.md
+// §9, r18).  They are used only once the leaf's box test has passed, so without this the compiler
+// sinks their loads behind that test: a second dependent round trip before the first triangle test
+// (MT's first operation needs e2).  An empty asm that reads them keeps the loads in the batch.
+__device__ __forceinline__ void issue_together(const float4 &a, const float4 &b, const float4 &c, const float4 &d,
+                                               const float4 &e, const float4 &f) {
+    asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(c.x), "v"(c.y),
+                 "v"(c.z), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w), "v"(e.x), "v"(e.y), "v"(e.z), "v"(f.x), "v"(f.y),
+                 "v"(f.z));
+}
+
 __device__ __forceinline__ bool is_internal(uint32_t c) { return !(c & AKR_CHILD_LEAF); }
 __device__ __forceinline__ bool is_leaf(uint32_t c) { return (c & AKR_CHILD_LEAF) && c != AKR_CHILD_EMPTY; }
 
@@ -682,6 +693,7 @@ __global__ __launch_bounds__(kTraceBlock) AKR_TRACE_ATTR void k_trace(TraceArgs 
                     pa1 = lr[5];
                     pb1 = lr[6];
                     pc1 = lr[7];
+                    issue_together(pa, pb, pc, pa1, pb1, pc1);
                     const float tl = box_test<TIGHT, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, o, invd, tmin, tmax);
                     const bool in = !(tl < 0.0f || tl > (ANY ? tmax : best));
                     if (COUNT) {
@@ -1381,6 +1393,7 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
             const float4 l0 = lr[0], l1 = lr[1];
             const float4 pa0 = lr[2], pb0 = lr[3], pc0 = lr[4];
             const float4 pa1 = lr[5], pb1 = lr[6], pc1 = lr[7];
+            issue_together(pa0, pb0, pc0, pa1, pb1, pc1);
             const float tl = box_test<true, true>(l0.x, l0.w, l0.y, l1.x, l0.z, l1.y, r.o, r.invd, r.tmin, r.tmax);
             const bool in = !(tl < 0.0f || tl > r.best);
             const uint32_t cnt = in ? fbits(l1.w) : 0u;
