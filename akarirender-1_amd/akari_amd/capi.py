@@ -492,7 +492,9 @@ class HipContext:
         """k_path phase profile of the counted launches since reset_stats (ticks: 100 MHz)."""
         keys = ("waves", "outer", "procs", "trav_iters", "t_proc", "t_trav", "t_leaf", "t_total", "t_max", "lanes_proc",
                 "t_shade", "spec_started", "spec_aborted", "tv_issue", "tv_wait", "tv_comp", "tl_issue", "tl_wait",
-                "tl_comp", "tp_park", "tp_next", "tp_begin", "tp_load", "leaf_phases", "leaf_holders")
+                "tl_comp", "tp_park", "tp_next", "tp_begin", "tp_load", "leaf_phases", "leaf_holders",
+                # option count_lines (k_path): distinct 128-B lines the last such render read, per region
+                "lines_nodes", "lines_leaves", "lines_shading")
         out = (C.c_uint64 * len(keys))()
         self._check(self.lib.akr_hip_path_profile(self.h, out, len(keys)))
         return dict(zip(keys, (int(v) for v in out)))

@@ -284,6 +284,8 @@ struct PathArgs {
     uint32_t gate_want;            //   candidate forms launched back to back, k_pick_form chose one)
     uint32_t probe_clock;          // diagnostic (counting build, option "pixel_probe" 2): the probe's flags
                                    // carry the pixel's completion time, (wall clock >> 4) << 8 | flags
+    uint32_t *lines;               // counting build, k_path, option "count_lines": bitmap of the 128-B lines
+    uint32_t lines_leaf, lines_shade;  // read (wide nodes from bit 0, the leaf blob, the shading records)
 };
 
 }  // namespace akr

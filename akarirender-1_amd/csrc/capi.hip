@@ -395,6 +395,11 @@ struct akr_hip_ctx {
     uint64_t n_steps = 0;
     DBuf<TraceCounters> d_counters;
     DBuf<PathProfile> d_pprof;  // k_path counting build: per-wave phase profile
+    // option count_lines (counting build, k_path): the bitmap of 128-B lines a render read, and the
+    // bit ranges of its three regions (wide nodes, leaf blob, shading records)
+    bool count_lines = false;
+    DBuf<uint32_t> d_lines;
+    uint32_t lines_span[4] = {0, 0, 0, 0};
     std::vector<hipEvent_t> pool;
     struct Pending {
         const char *name;
@@ -1026,6 +1031,21 @@ struct akr_hip_ctx {
                 pa.max_depth = p.max_depth;
                 pa.ray_clamp = p.ray_clamp;
                 pa.prof = count ? d_pprof.p : nullptr;
+                if (count && count_lines) {
+                    auto span = [](const void *p, size_t bytes) {
+                        const uint64_t a = (uint64_t)p;
+                        return (uint32_t)(bytes ? ((a + bytes - 1) >> 7) - (a >> 7) + 1 : 0);
+                    };
+                    lines_span[0] = 0;
+                    lines_span[1] = span(d_wnodes.p, d_wnodes.n * sizeof(akr_bvh4_node));
+                    lines_span[2] = lines_span[1] + span(d_wleaves.p, d_wleaves.n * sizeof(float4));
+                    lines_span[3] = lines_span[2] + span(d_shade_tri.p, d_shade_tri.n * sizeof(ShadeTri));
+                    d_lines.reserve(lines_span[3] / 32 + 1);
+                    HIPCHK(hipMemsetAsync(d_lines.p, 0, (lines_span[3] / 32 + 1) * sizeof(uint32_t), ms));
+                    pa.lines = d_lines.p;
+                    pa.lines_leaf = lines_span[1];
+                    pa.lines_shade = lines_span[2];
+                }
                 pa.probe = probe_p;
                 pa.fault = d_fault_host;
                 pa.fault_test = fault_test ? 1u : 0u;
@@ -1387,6 +1407,8 @@ int akr_hip_set_option(akr_hip_ctx *ctx, const char *key, int64_t value) {
             ctx->exact_cull = value != 0;
         } else if (k == "count_tests") {
             ctx->count = value != 0;
+        } else if (k == "count_lines") {  // with count_tests: k_path marks the 128-B lines it reads
+            ctx->count_lines = value != 0;
         } else if (k == "ray_steps") {
             ctx->ray_steps = value != 0;
         } else if (k == "wide") {
@@ -2145,10 +2167,19 @@ int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n) {
         if (!out || n < 0) throw std::runtime_error("null output");
         PathProfile q{};
         if (ctx->d_pprof.p) HIPCHK(hipMemcpy(&q, ctx->d_pprof.p, sizeof(q), hipMemcpyDeviceToHost));
-        const uint64_t v[] = {q.waves, q.outer, q.procs, q.trav_iters, q.t_proc, q.t_trav, q.t_leaf, q.t_total, q.t_max,
-                              q.lanes_proc, q.t_shade, q.spec_started, q.spec_aborted, q.tv_issue, q.tv_wait,
-                              q.tv_comp, q.tl_issue, q.tl_wait, q.tl_comp, q.tp_park, q.tp_next, q.tp_begin, q.tp_load,
-                              q.leaf_phases, q.leaf_holders};
+        uint64_t v[] = {q.waves, q.outer, q.procs, q.trav_iters, q.t_proc, q.t_trav, q.t_leaf, q.t_total, q.t_max,
+                        q.lanes_proc, q.t_shade, q.spec_started, q.spec_aborted, q.tv_issue, q.tv_wait,
+                        q.tv_comp, q.tl_issue, q.tl_wait, q.tl_comp, q.tp_park, q.tp_next, q.tp_begin, q.tp_load,
+                        q.leaf_phases, q.leaf_holders, 0, 0, 0};
+        // out[25..27]: distinct 128-B lines of the wide nodes, the leaf blob and the shading records the
+        // last render with count_lines read (k_path)
+        if (n > 25 && ctx->count_lines && ctx->d_lines.p && ctx->lines_span[3]) {
+            std::vector<uint32_t> m(ctx->lines_span[3] / 32 + 1);
+            HIPCHK(hipMemcpy(m.data(), ctx->d_lines.p, m.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            for (int r = 0; r < 3; r++)
+                for (uint32_t b = ctx->lines_span[r]; b < ctx->lines_span[r + 1]; b++)
+                    v[25 + r] += (m[b >> 5] >> (b & 31u)) & 1u;
+        }
         for (int32_t k = 0; k < n && k < (int32_t)(sizeof(v) / sizeof(v[0])); k++) out[k] = v[k];
     });
 }

@@ -1282,7 +1282,23 @@ struct PathCount {
     // leaf phases entered with at least one lane holding a leaf, and those lanes summed
     unsigned long long lphases = 0, lholders = 0;
     bool deep_now = false;
+    // option count_lines (k_path): the bitmap of 128-B lines read, wide nodes from bit 0, the leaf blob
+    // from bit lines_leaf (distinct lines per sample pass against the fabric reads)
+    uint32_t *lines = nullptr;
+    uint32_t lines_leaf = 0;
+    const float4 *leaf_base = nullptr;
 };
+
+// Counting build, option count_lines: marks the 128-B lines of [p, p + bytes) in the bitmap, as bit
+// base + (line index within the region that starts at `region`)
+__device__ __forceinline__ void mark_lines(uint32_t *map, uint32_t base, const void *region, const void *p,
+                                           uint32_t bytes) {
+    const uint64_t r0 = (uint64_t)region >> 7, a = (uint64_t)p;
+    for (uint64_t l = (a >> 7) - r0; l <= ((a + bytes - 1) >> 7) - r0; l++) {
+        const uint32_t b = base + (uint32_t)l;
+        atomicOr(map + (b >> 5), 1u << (b & 31u));
+    }
+}
 
 // B. k_trace's traversal phase over every busy lane's ray (all rays here are lean)
 template <bool COUNT>
@@ -1313,6 +1329,7 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
                 c.box[kind] += nt;
                 c.visit[kind]++;
                 c.deep_now = c.deep_now || r.sp > kStackLds;
+                if (c.lines) mark_lines(c.lines, 0u, wn, reinterpret_cast<const char *>(wn) + ((size_t)r.cur << 6), 64u);
             }
         } else if (busy && is_internal(r.cur)) {
             const WideNode nd = wide_load(wn, r.cur);
@@ -1361,7 +1378,10 @@ __device__ __forceinline__ bool leaf_tests(int kind, PathRay &r, const float4 *l
         const float4 ta = k == 0 ? pa0 : (k == 1 ? pa1 : tp[3 * k + 0]);
         const float4 tb = k == 0 ? pb0 : (k == 1 ? pb1 : tp[3 * k + 1]);
         const float4 tc = k == 0 ? pc0 : (k == 1 ? pc1 : tp[3 * k + 2]);
-        if (COUNT) c.tri[kind]++;
+        if (COUNT) {
+            c.tri[kind]++;
+            if (c.lines && k >= 2) mark_lines(c.lines, c.lines_leaf, c.leaf_base, tp + 3 * k, 48u);
+        }
         float t, u, v;
         if (mt(r.o, r.d, r.tmin, r.tmax, ta, tb, tc, r.best, t, u, v)) {
             r.best = t;
@@ -1431,6 +1451,7 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
         const unsigned long long tb = wall_clock64();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long tc = wall_clock64();
+        if (in_leaf && c.lines) mark_lines(c.lines, c.lines_leaf, wide_leaves, lr, 128u);
         if (in_leaf) hit_any = leaf_tests<true>(kind, r, lr, l0, l1, pa0, pb0, pc0, pa1, pb1, pc1, c);
         c.tl_issue += tb - ta;
         c.tl_wait += tc - tb;
@@ -1652,6 +1673,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     const bool ff = a.any_far_first != 0;
     const auto tab = PathTab<TAB>::make(pa.sc, s_tab);  // one workgroup barrier when TAB
     PathCount c;
+    if (COUNT) {
+        c.lines = pa.lines;
+        c.lines_leaf = pa.lines_leaf;
+        c.leaf_base = a.wide_leaves;
+    }
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
     f.s_lo = shard_begin(n, f.shard);
     f.s_hi = shard_begin(n, f.shard + 1);
@@ -1723,6 +1749,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                 } else {
                     const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
                     Bounce bo;
+                    if (COUNT && pa.lines)
+                        mark_lines(pa.lines, pa.lines_shade, pa.sc.tri, pa.sc.tri + hgid, (uint32_t)sizeof(ShadeTri));
                     // inlined: 3 % faster than an out-of-line call once every load is global
                     shade_hit_tab(pa.sc, tab, hgid, r.bu, r.bv, wo, beta, seed, depth,
                               pa.max_depth, depth == nb - 1, bo, COUNT ? &tl_phase : nullptr);

@@ -438,6 +438,8 @@ def main():
                     help="library option (akr_hip_set_option), repeatable; tuning / A-B only")
     ap.add_argument("--wavefront-spp", type=int, default=16,
                     help="untimed same-run leg in the wavefront form (north_star's layout), spp; 0 = skip")
+    ap.add_argument("--count-lines", type=int, default=1,
+                    help="1: an untimed 1-spp pass counting the distinct 128-B lines k_path reads (roofline.lines_per_pass)")
     ap.add_argument("--side-legs", type=int, default=1,
                     help="N = 1, soup: also render C2 (Cornell 1080p, 1024 spp) and the C4 stand-in (hall 4K, 256 spp) "
                          "as untimed legs of the same run (the line's `configs` block); 0 = skip")
@@ -562,6 +564,17 @@ def main():
     counts = ctx.trace_counts()
     cstats = ctx.kernel_stats()
     pprof = ctx.path_profile()   # the counting build's phase clocks (persistent forms only)
+    lines = None
+    if pprof.get("waves") and args.count_lines:
+        # distinct 128-B lines one sample pass reads, in a pass of its own: k_path's
+        # counting build marks every node / leaf / shading-record line in a bitmap (atomics: the clocks
+        # of the pass above stay clean)
+        ctx.set_option("count_lines", 1)
+        ctx.render_device(1, args.max_depth, tiles, rad.data_ptr(), wgt.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        lp = ctx.path_profile()
+        ctx.set_option("count_lines", 0)
+        lines = {k: lp[f"lines_{k}"] for k in ("nodes", "leaves", "shading")}
     ctx.set_option("count_tests", 0)
     ctx.reset_stats()
     # events around every launch cost nothing on a whole frame but ~6 % of an 8-way rank's step;
@@ -741,6 +754,16 @@ def main():
         roofline["latency"] = latency_model(prof, cl, sh, npix, value * 1e6)
     if dom == "path":
         roofline["time_split"] = time_split(pprof, counts)
+    if lines:
+        # the fabric's reads per sample pass against the distinct lines a pass touches: how often a line
+        # is fetched again within a pass
+        distinct = 128 * sum(lines.values())
+        fabric = read_traffic / spp if (read_traffic and dom == "path") else None
+        roofline["lines_per_pass"] = {**{k + "_gb": round(128 * v / 1e9, 4) for k, v in lines.items()},
+                                      "distinct_gb": round(distinct / 1e9, 4),
+                                      "fabric_read_gb": round(fabric / 1e9, 4) if fabric else None,
+                                      "fabric_over_distinct": round(fabric / distinct, 2) if fabric and distinct else None,
+                                      "source": "counting build, untimed 1-spp k_path pass, bitmap of 128-B lines"}
     if achieved > HBM_PEAK_GBS:   # the model bytes are not HBM bytes: caches serve most of them
         roofline["note"] = ("the SURVEY.md §8d algorithmic bytes exceed the HBM peak: most node and triangle reads "
                             "hit L2 or the Infinity Cache (on C3 ~66 % L2 hits by PMC, profiles/r20g_summary.md; a small scene's BVH is wholly "

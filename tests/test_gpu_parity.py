@@ -565,6 +565,34 @@ def test_path_pilot_order_bit_exact(hip_ctx_factory, defer):
             ctx.set_option("count_tests", 0)
 
 
+def test_count_lines_bitmap(hip_ctx_factory):
+    """Option count_lines (bench.py roofline.lines_per_pass): k_path's counting build
+    marks the 128-B lines it reads.  The render stays bit-exact; every region has lines marked; a 64-B
+    node lies in one line, so the node lines are at most the node visits; every hit reads one 80-B
+    shading record (at most two lines); a render of a sub-tile marks no more lines than the whole frame."""
+    with hip_ctx_factory(0) as ctx:
+        for k, v in (("path", 1), ("path_defer", 0), ("path_spec", 0), ("path_order", 0)):
+            ctx.set_option(k, v)
+        cs, orc = _setup(ctx, small_soup(20_000, (48, 27)))
+        got = []
+        try:
+            ctx.set_option("count_tests", 1)
+            ctx.set_option("count_lines", 1)
+            for tiles in ([(0, 0, 48, 27)], [(5, 3, 13, 9)]):
+                ctx.reset_stats()
+                _check_render(ctx, orc, 1, 5, tiles, 48, 27)
+                got.append((ctx.path_profile(), ctx.trace_counts()["per_mode"]))
+        finally:
+            ctx.set_option("count_lines", 0)
+            ctx.set_option("count_tests", 0)
+        (full, fc), (sub, _) = got
+        for k in ("lines_nodes", "lines_leaves", "lines_shading"):
+            assert 0 < sub[k] <= full[k], (k, sub[k], full[k])
+        assert full["lines_nodes"] <= fc["closest"]["visits"] + fc["shadow"]["visits"]
+        assert full["lines_shading"] <= 2 * fc["closest"]["rays"]
+        assert full["lines_shading"] * 128 <= cs.n_tris * 80 + 256
+
+
 def test_spec_and_order_options_are_validated(hip_ctx_factory):
     """The speculative form's and the cost order's options reject values outside their ranges
     (akr_hip_set_option returns an error and leaves the option as it was), and accept their ends."""
