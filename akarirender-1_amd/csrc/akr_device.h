@@ -285,7 +285,8 @@ struct PathArgs {
     uint32_t probe_clock;          // diagnostic (counting build, option "pixel_probe" 2): the probe's flags
                                    // carry the pixel's completion time, (wall clock >> 4) << 8 | flags
     uint32_t *lines;               // counting build, k_path, option "count_lines": bitmap of the 128-B lines
-    uint32_t lines_leaf, lines_shade;  // read (wide nodes from bit 0, the leaf blob, the shading records)
+    uint32_t lines_span[4];        // read; bit ranges [span[r], span[r + 1]) of the wide nodes, the leaf blob
+                                   // and the shading records
 };
 
 }  // namespace akr

@@ -1043,8 +1043,7 @@ struct akr_hip_ctx {
                     d_lines.reserve(lines_span[3] / 32 + 1);
                     HIPCHK(hipMemsetAsync(d_lines.p, 0, (lines_span[3] / 32 + 1) * sizeof(uint32_t), ms));
                     pa.lines = d_lines.p;
-                    pa.lines_leaf = lines_span[1];
-                    pa.lines_shade = lines_span[2];
+                    for (int r = 0; r < 4; r++) pa.lines_span[r] = lines_span[r];
                 }
                 pa.probe = probe_p;
                 pa.fault = d_fault_host;

@@ -1282,21 +1282,24 @@ struct PathCount {
     // leaf phases entered with at least one lane holding a leaf, and those lanes summed
     unsigned long long lphases = 0, lholders = 0;
     bool deep_now = false;
-    // option count_lines (k_path): the bitmap of 128-B lines read, wide nodes from bit 0, the leaf blob
-    // from bit lines_leaf (distinct lines per sample pass against the fabric reads)
+    // option count_lines (k_path): the bitmap of 128-B lines read, wide nodes in bits [0, span[1]), the
+    // leaf blob in [span[1], span[2]) (distinct lines per sample pass against the
+    // fabric reads)
     uint32_t *lines = nullptr;
-    uint32_t lines_leaf = 0;
+    uint32_t span[3] = {0, 0, 0};
     const float4 *leaf_base = nullptr;
 };
 
-// Counting build, option count_lines: marks the 128-B lines of [p, p + bytes) in the bitmap, as bit
-// base + (line index within the region that starts at `region`)
-__device__ __forceinline__ void mark_lines(uint32_t *map, uint32_t base, const void *region, const void *p,
+// Counting build, option count_lines: marks the 128-B lines of [p, p + bytes) (bytes <= 128) in the
+// bitmap, line l of the region that starts at `region` as bit lo + l; a bit outside [lo, hi) is never
+// written
+__device__ __forceinline__ void mark_lines(uint32_t *map, uint32_t lo, uint32_t hi, const void *region, const void *p,
                                            uint32_t bytes) {
     const uint64_t r0 = (uint64_t)region >> 7, a = (uint64_t)p;
+    if (a < (uint64_t)region) return;
     for (uint64_t l = (a >> 7) - r0; l <= ((a + bytes - 1) >> 7) - r0; l++) {
-        const uint32_t b = base + (uint32_t)l;
-        atomicOr(map + (b >> 5), 1u << (b & 31u));
+        const uint64_t b = lo + l;
+        if (b < hi) atomicOr(map + (b >> 5), 1u << (b & 31u));
     }
 }
 
@@ -1324,12 +1327,14 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
             c.tv_issue += tb - ta;
             c.tv_wait += tc - tb;
             if (vis) {
+                const uint32_t node = r.cur;  // the visit moves r.cur on
                 const int nt = visit_wide_lean_node<false, true>(nd, r.cur, r.o, r.dpos, r.invd, r.tmin, r.tmaxp, r.best,
                                                                  s_stack, ovf, ovf_threads, tid, gtid, r.sp, &need_pop);
                 c.box[kind] += nt;
                 c.visit[kind]++;
                 c.deep_now = c.deep_now || r.sp > kStackLds;
-                if (c.lines) mark_lines(c.lines, 0u, wn, reinterpret_cast<const char *>(wn) + ((size_t)r.cur << 6), 64u);
+                if (c.lines)
+                    mark_lines(c.lines, 0u, c.span[1], wn, reinterpret_cast<const char *>(wn) + ((size_t)node << 6), 64u);
             }
         } else if (busy && is_internal(r.cur)) {
             const WideNode nd = wide_load(wn, r.cur);
@@ -1380,7 +1385,7 @@ __device__ __forceinline__ bool leaf_tests(int kind, PathRay &r, const float4 *l
         const float4 tc = k == 0 ? pc0 : (k == 1 ? pc1 : tp[3 * k + 2]);
         if (COUNT) {
             c.tri[kind]++;
-            if (c.lines && k >= 2) mark_lines(c.lines, c.lines_leaf, c.leaf_base, tp + 3 * k, 48u);
+            if (c.lines && k >= 2) mark_lines(c.lines, c.span[1], c.span[2], c.leaf_base, tp + 3 * k, 48u);
         }
         float t, u, v;
         if (mt(r.o, r.d, r.tmin, r.tmax, ta, tb, tc, r.best, t, u, v)) {
@@ -1451,7 +1456,7 @@ __device__ __forceinline__ bool path_leaf(bool busy, int kind, PathRay &r, const
         const unsigned long long tb = wall_clock64();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long tc = wall_clock64();
-        if (in_leaf && c.lines) mark_lines(c.lines, c.lines_leaf, wide_leaves, lr, 128u);
+        if (in_leaf && c.lines) mark_lines(c.lines, c.span[1], c.span[2], wide_leaves, lr, 128u);
         if (in_leaf) hit_any = leaf_tests<true>(kind, r, lr, l0, l1, pa0, pb0, pc0, pa1, pb1, pc1, c);
         c.tl_issue += tb - ta;
         c.tl_wait += tc - tb;
@@ -1675,7 +1680,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
     PathCount c;
     if (COUNT) {
         c.lines = pa.lines;
-        c.lines_leaf = pa.lines_leaf;
+        c.span[1] = pa.lines_span[1];
+        c.span[2] = pa.lines_span[2];
         c.leaf_base = a.wide_leaves;
     }
     PixelFetch f{blockIdx.x % kWorkShards, 0, 0, (int)kWorkShards, n == 0};
@@ -1750,7 +1756,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
                     const V3 wo{-bitsf(s_park[3][tid]), -bitsf(s_park[4][tid]), -bitsf(s_park[5][tid])};
                     Bounce bo;
                     if (COUNT && pa.lines)
-                        mark_lines(pa.lines, pa.lines_shade, pa.sc.tri, pa.sc.tri + hgid, (uint32_t)sizeof(ShadeTri));
+                        mark_lines(pa.lines, pa.lines_span[2], pa.lines_span[3], pa.sc.tri, pa.sc.tri + hgid,
+                                   (uint32_t)sizeof(ShadeTri));
                     // inlined: 3 % faster than an out-of-line call once every load is global
                     shade_hit_tab(pa.sc, tab, hgid, r.bu, r.bv, wo, beta, seed, depth,
                               pa.max_depth, depth == nb - 1, bo, COUNT ? &tl_phase : nullptr);

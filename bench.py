@@ -565,7 +565,7 @@ def main():
     cstats = ctx.kernel_stats()
     pprof = ctx.path_profile()   # the counting build's phase clocks (persistent forms only)
     lines = None
-    if pprof.get("waves") and args.count_lines:
+    if pprof.get("waves") and args.count_lines and world == 1:
         # distinct 128-B lines one sample pass reads, in a pass of its own: k_path's
         # counting build marks every node / leaf / shading-record line in a bitmap (atomics: the clocks
         # of the pass above stay clean)
