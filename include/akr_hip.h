@@ -208,6 +208,7 @@ int akr_hip_create(int device, akr_hip_ctx **out);
 int akr_hip_destroy(akr_hip_ctx *ctx);
 const char *akr_hip_last_error(const akr_hip_ctx *ctx);
 /* Options: "stats" (per-kernel HIP-event timing: 0 off, 1 every kernel, 2 trace_closest only), "count_tests" (traversal counters),
+ * "count_lines" (with count_tests: k_path marks the 128-B lines it reads, see akr_hip_path_profile),
  * "exact_cull", "wide", "lean", "shadow_grid_pct", "rays_per_lane" (tuning / A-B).
  * Render forms and their tuning (all give the same bits): "path" (0 wavefront,
  * 1 persistent kernel, 2 auto), "path_auto_pixels", "path_auto_complex";
@@ -316,7 +317,9 @@ int akr_hip_trace_counts(akr_hip_ctx *ctx, akr_trace_counts *out);
  * traversal and leaf phases: ticks issuing their loads, waiting for them, working after them, then
  * k_path's processing split: the park, the sample end with splat / pixel fetch / camera ray, and the
  * unpark with the new rays' start, and the shading's wait for the hit's record (out[19..22]),
- * then the leaf phases entered with a leaf held and the lanes holding one, summed (out[23..24]).
+ * then the leaf phases entered with a leaf held and the lanes holding one, summed (out[23..24]), then
+ * the distinct 128-B lines of the wide nodes, the leaf blob and the shading records that the last
+ * k_path render with "count_lines" read (out[25..27]).
  * Not part of the reference interface. */
 int akr_hip_path_profile(akr_hip_ctx *ctx, uint64_t *out, int32_t n);
 int akr_hip_reset_stats(akr_hip_ctx *ctx);
