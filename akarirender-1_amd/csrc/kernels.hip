@@ -1304,7 +1304,7 @@ __device__ __forceinline__ void mark_lines(uint32_t *map, uint32_t lo, uint32_t 
 }
 
 // B. k_trace's traversal phase over every busy lane's ray (all rays here are lean)
-template <bool COUNT>
+template <bool COUNT, int EXIT = kWhileExit>  // EXIT: the phase ends when <= EXIT lanes still search
 __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, const float4 *wn, lds_u64 *s_stack,
                                               glb_u64 *ovf, uint32_t ovf_threads, uint32_t tid, uint32_t gtid,
                                               PathCount &c) {
@@ -1353,11 +1353,11 @@ __device__ __forceinline__ void path_traverse(bool busy, int kind, PathRay &r, c
         if (need_pop) r.cur = stack_pop(s_stack, ovf, ovf_threads, tid, gtid, r.sp, r.best);
         const unsigned long long searching = __ballot(busy && r.leaf == AKR_CHILD_EMPTY && r.cur != AKR_CHILD_EMPTY);
         if constexpr (COUNT) {
-            const bool stop = (uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+            const bool stop = (uint32_t)__popcll(searching) <= (uint32_t)EXIT &&
                               (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0);
             c.tv_comp += wall_clock64() - tc;
             if (stop) break;
-        } else if ((uint32_t)__popcll(searching) <= (uint32_t)kWhileExit &&
+        } else if ((uint32_t)__popcll(searching) <= (uint32_t)EXIT &&
                    (searching == 0 || __ballot(busy && r.leaf != AKR_CHILD_EMPTY) != 0)) {
             break;
         }
@@ -1855,7 +1855,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         if (!__any(busy)) continue;
         // ---- B. traversal phase, C. leaf phase (k_trace's, shared with k_path_defer)
         const int kd = any ? 1 : 0;
-        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
+        path_traverse<COUNT, kWhileExitPath>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
         if (COUNT) {
             const unsigned long long t = wall_clock64();
             p_tt += t - p_t;
