@@ -54,7 +54,7 @@ constexpr int kRefillMinAny = AKR_REFILL_MIN_ANY;  // the same for occlusion (an
 constexpr uint64_t kMaxWideNodes = 1ull << 26;  // 64-B wide nodes addressed by a 32-bit byte offset (visit_wide_lean)
 constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this many lanes still search
 #ifndef AKR_WHILE_EXIT_PATH
-#define AKR_WHILE_EXIT_PATH AKR_WHILE_EXIT
+#define AKR_WHILE_EXIT_PATH 16  // k_path: 4.034-4.064 against 4.060-4.078 ms per spp at 12, 20 slower (profiles/r24/path_exit_ab.log)
 #endif
 constexpr int kWhileExitPath = AKR_WHILE_EXIT_PATH;  // the same for k_path alone (the other persistent forms keep kWhileExit)
 constexpr int kWhileExitAny = AKR_WHILE_EXIT_ANY;  // the same for occlusion traces
