@@ -57,6 +57,10 @@ constexpr int kWhileExit = AKR_WHILE_EXIT;  // traversal phase ends when <= this
 #define AKR_WHILE_EXIT_PATH 16  // k_path: 4.034-4.064 against 4.060-4.078 ms per spp at 12, 20 slower (profiles/r24/path_exit_ab.log)
 #endif
 constexpr int kWhileExitPath = AKR_WHILE_EXIT_PATH;  // the same for k_path alone (the other persistent forms keep kWhileExit)
+#ifndef AKR_WHILE_EXIT_SPEC
+#define AKR_WHILE_EXIT_SPEC AKR_WHILE_EXIT
+#endif
+constexpr int kWhileExitSpec = AKR_WHILE_EXIT_SPEC;  // the same for k_path_spec
 constexpr int kWhileExitAny = AKR_WHILE_EXIT_ANY;  // the same for occlusion traces
 #ifndef AKR_WORK_SHARDS
 #define AKR_WORK_SHARDS 8

@@ -2692,7 +2692,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(AKR
         idle_rounds = 0;
         // ---- B. traversal phase, C. leaf phase (k_trace's, shared with the other persistent kernels)
         const int kd = s.any() ? 1 : 0;
-        path_traverse<COUNT>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
+        path_traverse<COUNT, kWhileExitSpec>(busy, kd, r, a.wide_nodes, s_stack, stack_ovf, a.ovf_threads, tid, gtid, c);
         if (COUNT) {
             const unsigned long long t = wall_clock64();
             p_tt += t - p_t;

@@ -40,7 +40,7 @@ def test_product_build_compiles_no_probe_or_ab_variant():
             hits = [i + 1 for i, ln in enumerate(f.read_text().splitlines()) if banned.search(ln)]
             assert not hits, f"{f.name}: probe / A-B switch at lines {hits}"
     # the only preprocessor conditionals left are the header guard of device code and tuning defaults
-    allowed = re.compile(r"#\s*(ifndef AKR_(TRACE_BLOCK|STACK_LDS|REFILL_MIN|REFILL_MIN_ANY|WHILE_EXIT|WHILE_EXIT_ANY|WHILE_EXIT_PATH|"
+    allowed = re.compile(r"#\s*(ifndef AKR_(TRACE_BLOCK|STACK_LDS|REFILL_MIN|REFILL_MIN_ANY|WHILE_EXIT|WHILE_EXIT_ANY|WHILE_EXIT_PATH|WHILE_EXIT_SPEC|"
                          r"WORK_SHARDS|TRACE_WAVES|PATH_WAVES|SHADE_BLOCK)\b|if defined\(__HIP_DEVICE_COMPILE__\)|"
                          r"if defined\(__HIPCC__\)|ifdef __HIPCC__)")
     for f in sorted(csrc.glob("*")):
